@@ -1,0 +1,85 @@
+"""ctypes binding of libcmve.so (the C ABI declared in include/cmve.h).
+
+The library is REQUIRED: importing this module without a built libcmve.so raises
+ImportError -- there is no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CMVE_LIB", os.path.join(_HERE, "libcmve.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libcmve.so not found at {LIB_PATH}: build it with `make -C cross-modal-video-engine_amd` "
+                      "(or __graft_entry__.build()); cmve has no CPU fallback")
+
+lib = C.CDLL(LIB_PATH)
+
+# ---- enums (include/cmve.h) ----
+CMVE_OK = 0
+CMVE_F32, CMVE_F64, CMVE_BF16, CMVE_I32, CMVE_I64 = 0, 1, 2, 3, 4
+SIM_BF16, SIM_BF16X3 = 0, 1
+DIR_ROW, DIR_COL = 1, 2
+ROW_ALIGN, DIM_ALIGN = 128, 64
+TOPK_MAX = 2048
+
+
+class Rows(C.Structure):
+    """``cmve_rows_t`` -- a packed embedding set (device pointers)."""
+    _fields_ = [
+        ("n", C.c_int64), ("d", C.c_int64), ("n_pad", C.c_int64), ("d_pad", C.c_int64),
+        ("hi", C.c_void_p), ("lo", C.c_void_p),
+        ("raw", C.c_void_p), ("raw_dtype", C.c_int32), ("_pad0", C.c_int32), ("raw_ld", C.c_int64),
+        ("inv_norm", C.c_void_p), ("err_hi", C.c_void_p), ("err_hilo", C.c_void_p), ("err_max", C.c_void_p),
+        ("eps", C.c_double),
+    ]
+
+
+_vp, _i32, _i64, _f32, _f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_float, C.c_double
+_P = C.POINTER
+
+SIGNATURES = {
+    "cmve_abi_version": (C.c_int, []),
+    "cmve_last_error": (C.c_char_p, []),
+    "cmve_create": (C.c_int, [C.c_int, _vp, _P(_vp)]),
+    "cmve_set_stream": (C.c_int, [_vp, _vp]),
+    "cmve_destroy": (C.c_int, [_vp]),
+    "cmve_pack_size": (C.c_int, [_i64, _i64, _P(_i64), _P(_i64)]),
+    "cmve_pack_rows": (C.c_int, [_vp, _P(Rows)]),
+    "cmve_l2norm_rows": (C.c_int, [_vp, _vp, _i32, _i64, _vp, _i32, _i64, _i64, _i64, _f64]),
+    "cmve_sim_store": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _f32, _f32, _vp, _i32, _i64]),
+    "cmve_gt_thresholds": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp]),
+    "cmve_rank_count": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _i64, _vp]),
+    "cmve_rank_mfma": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                 _vp]),
+    "cmve_rank_fixup": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "cmve_rank_thresholds": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp]),
+    "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "cmve_topk": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)  # AttributeError here = a declared symbol is not exported
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+if lib.cmve_abi_version() != 1:
+    raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != 1")
+
+
+class CmveError(RuntimeError):
+    pass
+
+
+def check(status, what=""):
+    if status != CMVE_OK:
+        msg = lib.cmve_last_error().decode(errors="replace")
+        raise CmveError(f"{what or 'cmve call'} failed with status {status}: {msg}")
+
+
+def exported_symbols():
+    return sorted(SIGNATURES)

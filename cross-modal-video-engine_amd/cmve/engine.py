@@ -1,0 +1,316 @@
+"""Device-side engine: packed embedding sets in HBM and the scoring / ranking calls.
+
+PyTorch-ROCm provides device memory and streams only; every computation is a
+libcmve.so (hand-written HIP, gfx950) call.  There is no CPU fallback: without a
+GPU every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import lib, check, Rows
+
+_HANDLES: Dict[Tuple[int, int], int] = {}
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("cmve needs a ROCm GPU (MI355X / gfx950); no CPU fallback exists")
+
+
+def default_device() -> torch.device:
+    require_gpu()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def handle(device: Optional[torch.device] = None) -> int:
+    """cmve handle bound to the CURRENT torch stream of `device`."""
+    device = device or default_device()
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    stream = torch.cuda.current_stream(idx).cuda_stream
+    key = (idx, stream)
+    h = _HANDLES.get(key)
+    if h is None:
+        out = C.c_void_p()
+        check(lib.cmve_create(idx, C.c_void_p(stream), C.byref(out)), "cmve_create")
+        h = out.value
+        _HANDLES[key] = h
+    return h
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return _lib.CMVE_F32
+    if t.dtype == torch.float64:
+        return _lib.CMVE_F64
+    raise TypeError(f"cmve: unsupported dtype {t.dtype} (float32 / float64 only)")
+
+
+def pack_size(n: int, d: int) -> Tuple[int, int]:
+    n_pad, d_pad = C.c_int64(), C.c_int64()
+    check(lib.cmve_pack_size(n, d, C.byref(n_pad), C.byref(d_pad)), "cmve_pack_size")
+    return n_pad.value, d_pad.value
+
+
+def to_device(x, device: Optional[torch.device] = None, dtype=None) -> torch.Tensor:
+    """numpy / torch -> contiguous float32|float64 device tensor (dtype preserved unless given)."""
+    device = device or default_device()
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    elif t.dtype in (torch.float16, torch.bfloat16):
+        t = t.to(torch.float32)
+    elif t.dtype not in (torch.float32, torch.float64):
+        t = t.to(torch.float64)
+    return t.to(device, non_blocking=True).contiguous()
+
+
+class RowSet:
+    """A packed, L2-normalised embedding set resident in HBM (``cmve_rows_t``).
+
+    ``eps=0`` reproduces LINAS ``l2norm`` (no epsilon, ``LINAS-engine/evaluation.py:10-14``);
+    ``eps=1e-12`` reproduces ``F.normalize`` (``MultiFusion/src/combiner.py:134``).
+    The raw rows are kept: the exact fp64 fix-up reads them.
+    """
+
+    def __init__(self, x, eps: float = 0.0, with_lo: bool = True, device: Optional[torch.device] = None):
+        device = device or default_device()
+        raw = to_device(x, device)
+        if raw.dim() != 2:
+            raise ValueError(f"RowSet expects a 2-D [n, d] matrix, got shape {tuple(raw.shape)}")
+        n, d = raw.shape
+        if d == 0:
+            raise ValueError("RowSet: zero-dimensional embeddings")
+        n_pad, d_pad = pack_size(n, d)
+        self.device = device
+        self.raw = raw
+        self.n, self.d, self.n_pad, self.d_pad = n, d, n_pad, d_pad
+        self.eps = float(eps)
+        self.hi = torch.empty((n_pad, d_pad), dtype=torch.int16, device=device)
+        self.lo = torch.empty((n_pad, d_pad), dtype=torch.int16, device=device) if with_lo else None
+        self.inv_norm = torch.empty(n_pad, dtype=torch.float64, device=device)
+        self.err_hi = torch.empty(n_pad, dtype=torch.float32, device=device)
+        self.err_hilo = torch.empty(n_pad, dtype=torch.float32, device=device)
+        self.err_max = torch.empty(2, dtype=torch.float32, device=device)
+        self.desc = Rows(n=n, d=d, n_pad=n_pad, d_pad=d_pad, hi=self.hi.data_ptr(),
+                         lo=self.lo.data_ptr() if self.lo is not None else None,
+                         raw=raw.data_ptr() if n else None, raw_dtype=_dtype_code(raw), _pad0=0,
+                         raw_ld=raw.stride(0) if n else d, inv_norm=self.inv_norm.data_ptr(),
+                         err_hi=self.err_hi.data_ptr(), err_hilo=self.err_hilo.data_ptr(),
+                         err_max=self.err_max.data_ptr(), eps=self.eps)
+        check(lib.cmve_pack_rows(handle(device), C.byref(self.desc)), "cmve_pack_rows")
+
+    @property
+    def has_lo(self):
+        return self.lo is not None
+
+    def normalized(self, dtype=torch.float64) -> torch.Tensor:
+        """x / max(||x||, eps) on device (K1')."""
+        out = torch.empty((self.n, self.d), dtype=dtype, device=self.device)
+        if self.n:
+            check(lib.cmve_l2norm_rows(handle(self.device), _ptr(self.raw), _dtype_code(self.raw), self.raw.stride(0),
+                                       _ptr(out), _dtype_code(out), out.stride(0), self.n, self.d, self.eps),
+                  "cmve_l2norm_rows")
+        return out
+
+
+def _mode_for(q: RowSet, g: RowSet, mode: Optional[int]) -> int:
+    if mode is None:
+        mode = _lib.SIM_BF16X3 if (q.has_lo and g.has_lo) else _lib.SIM_BF16
+    if mode == _lib.SIM_BF16X3 and not (q.has_lo and g.has_lo):
+        raise ValueError("BF16X3 mode needs both sets packed with lo planes")
+    return mode
+
+
+def sim_store(q: RowSet, g: RowSet, alpha: float = 1.0, beta: float = 0.0, mode: Optional[int] = None,
+              out_dtype=torch.float32) -> torch.Tensor:
+    """out[i, j] = alpha * cos(q_i, g_j) + beta on device."""
+    mode = _mode_for(q, g, mode)
+    out = torch.empty((q.n, g.n), dtype=out_dtype, device=q.device)
+    if q.n and g.n:
+        check(lib.cmve_sim_store(handle(q.device), C.byref(q.desc), C.byref(g.desc), mode, alpha, beta, _ptr(out),
+                                 _dtype_code(out), out.stride(0)), "cmve_sim_store")
+    return out
+
+
+def csr(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Python GT lists -> (offsets int64 [n+1], indices int32) device tensors."""
+    lens = np.fromiter((len(l) for l in lists), dtype=np.int64, count=len(lists))
+    off = np.zeros(len(lists) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    idx = np.fromiter((int(v) for l in lists for v in l), dtype=np.int32, count=int(off[-1]))
+    if idx.size == 0:
+        idx = np.zeros(1, np.int32)
+    return (torch.from_numpy(off).to(device), torch.from_numpy(idx).to(device))
+
+
+def gt_thresholds(a: RowSet, b: RowSet, off: torch.Tensor, idx: torch.Tensor, mode: int):
+    sgt = torch.empty(a.n_pad, dtype=torch.float64, device=a.device)
+    hi = torch.empty(a.n_pad, dtype=torch.float32, device=a.device)
+    lo = torch.empty(a.n_pad, dtype=torch.float32, device=a.device)
+    check(lib.cmve_gt_thresholds(handle(a.device), C.byref(a.desc), C.byref(b.desc), mode, _ptr(off), _ptr(idx),
+                                 _ptr(sgt), _ptr(hi), _ptr(lo)), "cmve_gt_thresholds")
+    return sgt, hi, lo
+
+
+class RankWorkspace:
+    """Reusable device buffers for rank_count (candidate list grows on overflow)."""
+
+    def __init__(self, device, cap: int = 1 << 20):
+        self.device = device
+        self.cand = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int64, device=device)
+
+    @property
+    def cap(self):
+        return self.cand.numel()
+
+    def grow(self, need: int):
+        self.cand = torch.empty(int(need * 1.25) + 1024, dtype=torch.int64, device=self.device)
+
+
+def rank_thresholds(a: RowSet, b: RowSet, sgt: torch.Tensor, mode: int):
+    """fp32 bracketing thresholds for given exact GT scores sgt[a.n_pad] (NaN = no GT)."""
+    hi = torch.empty(a.n_pad, dtype=torch.float32, device=a.device)
+    lo = torch.empty(a.n_pad, dtype=torch.float32, device=a.device)
+    check(lib.cmve_rank_thresholds(handle(a.device), C.byref(a.desc), C.byref(b.desc), mode, _ptr(sgt), _ptr(hi),
+                                   _ptr(lo)), "cmve_rank_thresholds")
+    return hi, lo
+
+
+def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: Optional[RankWorkspace] = None,
+                      row_cnt=None, col_cnt=None, events=None):
+    """Enqueue the fused rank count (no sync).  row/col = (sgt, thr_hi, thr_lo) or None.
+    events = (start, mid, end) torch.cuda.Event triple recorded around the MFMA pass and the fix-up."""
+    dirs = (_lib.DIR_ROW if row is not None else 0) | (_lib.DIR_COL if col is not None else 0)
+    if row is not None and row_cnt is None:
+        row_cnt = torch.empty(q.n_pad, dtype=torch.int32, device=q.device)
+    if col is not None and col_cnt is None:
+        col_cnt = torch.empty(g.n_pad, dtype=torch.int32, device=q.device)
+    r = row if row is not None else (None, None, None)
+    c = col if col is not None else (None, None, None)
+    h = handle(q.device)
+    if events is not None:
+        events[0].record()
+    check(lib.cmve_rank_mfma(h, C.byref(q.desc), C.byref(g.desc), mode, dirs, _ptr(r[1]), _ptr(r[2]), _ptr(c[1]),
+                             _ptr(c[2]), _ptr(row_cnt), _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)),
+          "cmve_rank_mfma")
+    if events is not None:
+        events[1].record()
+    check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(row_cnt),
+                              _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)), "cmve_rank_fixup")
+    if events is not None:
+        events[2].record()
+    return row_cnt, col_cnt
+
+
+def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int = _lib.SIM_BF16,
+                   ws: Optional[RankWorkspace] = None):
+    """Exact GT ranks in both directions from ONE fused GEMM pass.
+
+    row_gts[i]: GT indices into g for query row i (t2v); col_gts[j]: GT indices into q
+    for gallery row j (v2t).  Returns (row_ranks, col_ranks, n_candidates) as numpy int64,
+    1-based; empty GT lists give n_other + 1 (``LINAS-engine/util/metrics.py:140``).
+    """
+    if row_gts is None and col_gts is None:
+        raise ValueError("gt_rank_counts: need row_gts and/or col_gts")
+    if mode == _lib.SIM_BF16X3 and not (q.has_lo and g.has_lo):
+        raise ValueError("BF16X3 needs lo planes")
+    ws = ws or RankWorkspace(q.device, cap=max(1 << 16, 64 * (q.n + g.n)))
+    row = col = None
+    if row_gts is not None:
+        roff, ridx = csr(row_gts, q.device)
+        row = gt_thresholds(q, g, roff, ridx, mode)
+    if col_gts is not None:
+        coff, cidx = csr(col_gts, q.device)
+        col = gt_thresholds(g, q, coff, cidx, mode)
+    for _attempt in range(4):
+        rc, cc = rank_count_launch(q, g, mode, row, col, ws)
+        ncand = int(ws.count.item())  # synchronises
+        if ncand <= ws.cap:
+            break
+        ws.grow(ncand)
+    else:
+        raise _lib.CmveError("rank_count: candidate list kept overflowing")
+    out_r = out_c = None
+    if row_gts is not None:
+        out_r = rc[:q.n].to(torch.int64).cpu().numpy() + 1
+        empty = np.fromiter((len(l) == 0 for l in row_gts), bool, count=len(row_gts))
+        out_r[empty] = g.n + 1
+    if col_gts is not None:
+        out_c = cc[:g.n].to(torch.int64).cpu().numpy() + 1
+        empty = np.fromiter((len(l) == 0 for l in col_gts), bool, count=len(col_gts))
+        out_c[empty] = q.n + 1
+    return out_r, out_c, ncand
+
+
+def rank_from_matrix(errors, gts, transposed: bool = False, device=None) -> np.ndarray:
+    """1-based GT ranks from a materialised error matrix (lower = better), on device."""
+    device = device or default_device()
+    e = to_device(errors, device)
+    n_rows, n_cols = e.shape
+    n_q = n_cols if transposed else n_rows
+    lists = [gts[i] if (not isinstance(gts, dict) or i in gts) else [] for i in range(n_q)]
+    off, idx = csr(lists, device)
+    cnt = torch.zeros(n_q, dtype=torch.int32, device=device)
+    check(lib.cmve_rank_from_matrix(handle(device), _ptr(e), _dtype_code(e), n_rows, n_cols, e.stride(0),
+                                    1 if transposed else 0, _ptr(off), _ptr(idx), _ptr(cnt)),
+          "cmve_rank_from_matrix")
+    ranks = cnt.to(torch.int64).cpu().numpy() + 1
+    n_m = n_rows if transposed else n_cols
+    empty = np.fromiter((len(l) == 0 for l in lists), bool, count=n_q)
+    ranks[empty] = n_m + 1
+    return ranks
+
+
+def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_BF16, scores_ws: Optional[torch.Tensor] = None):
+    """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines."""
+    k = int(min(k, g.n))
+    if k < 1:
+        return np.zeros((q.n, 0), np.int64), np.zeros((q.n, 0))
+    if k > _lib.TOPK_MAX:
+        raise ValueError(f"topk: k <= {_lib.TOPK_MAX}")
+    if scores_ws is None or scores_ws.numel() < q.n_pad * g.n_pad:
+        scores_ws = torch.empty(q.n_pad * g.n_pad, dtype=torch.float32, device=q.device)
+    idx = torch.empty((max(q.n, 1), k), dtype=torch.int32, device=q.device)
+    sc = torch.empty((max(q.n, 1), k), dtype=torch.float64, device=q.device)
+    ovf = torch.zeros(1, dtype=torch.int32, device=q.device)
+    for m in ((mode, _lib.SIM_BF16X3) if (mode == _lib.SIM_BF16 and q.has_lo and g.has_lo) else (mode,)):
+        check(lib.cmve_topk(handle(q.device), C.byref(q.desc), C.byref(g.desc), m, k, _ptr(scores_ws), _ptr(idx),
+                            _ptr(sc), _ptr(ovf)), "cmve_topk")
+        if int(ovf.item()) == 0:
+            break
+    else:
+        raise _lib.CmveError("topk: the error band kept more than 4096 columns for some query")
+    return idx[:q.n].to(torch.int64).cpu().numpy(), sc[:q.n].cpu().numpy()
+
+
+def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_BF16):
+    """Exact 1-based position of EVERY GT item: for row i of `a` and k in lists[i],
+    1 + #{j : cos64(a_i, b_j) > cos64(a_i, b_k)}.  Implemented as a fused rank count
+    over an expanded query set (row i repeated once per GT item, GT list [k])."""
+    owners = np.fromiter((i for i, l in enumerate(lists) for _ in l), dtype=np.int64)
+    items = [[int(k)] for l in lists for k in l]
+    out = [np.zeros(0, np.int64) for _ in lists]
+    if owners.size == 0:
+        return out
+    sel = torch.from_numpy(owners).to(a.device)
+    expanded = RowSet(a.raw.index_select(0, sel), eps=a.eps, with_lo=a.has_lo, device=a.device)
+    r, _, _ = gt_rank_counts(expanded, b, row_gts=items, mode=mode)
+    p = 0
+    for i, l in enumerate(lists):
+        out[i] = r[p:p + len(l)]
+        p += len(l)
+    return out

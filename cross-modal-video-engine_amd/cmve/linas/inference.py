@@ -1,0 +1,82 @@
+"""Drop-in mirror of the ``LINAS-engine/inference.py`` gallery scorer + CLI.
+
+Reference hot loop (inference.py:76-82):
+    errors = evaluation.cal_error(video_embs, cap_emb, options.measure)   # re-normalises the gallery
+    inds = np.argsort(errors[0])[:opt.topK]                               # full O(N log N) sort
+    print([video_ids[i] for i in inds])
+Here the gallery is normalised and packed into HBM ONCE (``GalleryScorer``) and each
+query batch is scored by the bf16 MFMA kernel with an exact fp64 top-k epilogue
+(``cmve_topk``): same ids, same order (score desc; ties by index) as the reference's
+argsort on tie-free scores.
+
+CLI (same flags as inference.py:37-44, plus the inputs the frozen encoder would make):
+  python -m cmve.linas.inference --input "a man ..." --topK 10 --gpu 0 \
+      --gallery video_data.npz --query-emb cap.npy
+``--gallery`` is an .npz with ``video_embs`` [N, D] and ``video_ids`` (the content of the
+reference's ``video_data.pt`` cache, inference.py:57-67); ``--query-emb`` is the caption
+embedding that ``model.embed_txt_distill(process_cap(input))`` produces (inference.py:76-77).
+The frozen biGRU text encoder needs the unshipped checkpoint
+``student_support_set_8/model_best.pth.tar`` (LINAS-engine/readme.md:17), so it is an input here.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+
+from .. import engine
+from .._lib import SIM_BF16
+
+
+class GalleryScorer:
+    """A video gallery resident in HBM, normalised once (LINAS l2norm, no eps)."""
+
+    def __init__(self, video_embs, video_ids=None, with_lo=True):
+        self.gallery = engine.RowSet(np.asarray(video_embs), eps=0.0, with_lo=with_lo)
+        self.video_ids = list(video_ids) if video_ids is not None else None
+        self._ws = None
+
+    def topk_indices(self, cap_embs, topK=10):
+        """[N_q, topK] gallery indices, best first (== np.argsort(cal_error(...)[i])[:topK])."""
+        cap_embs = np.atleast_2d(np.asarray(cap_embs))
+        q = engine.RowSet(cap_embs, eps=0.0, with_lo=self.gallery.has_lo, device=self.gallery.device)
+        need = q.n_pad * self.gallery.n_pad
+        if self._ws is None or self._ws.numel() < need:
+            import torch
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.gallery.device)
+        idx, _ = engine.topk(q, self.gallery, topK, mode=SIM_BF16, scores_ws=self._ws)
+        return idx
+
+    def topk_ids(self, cap_emb, topK=10):
+        inds = self.topk_indices(cap_emb, topK)[0]
+        return [self.video_ids[i] for i in inds]
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument('--input', default='a man and a woman is talking.', type=str, help='input sentence')
+    p.add_argument('--topK', default=10, type=int, help='return top-k videos')
+    p.add_argument('--gpu', default='0', type=str, help='gpu device')
+    p.add_argument('--gallery', default='video_data.npz', type=str,
+                   help='npz with video_embs [N,D] and video_ids (the video_data.pt cache content)')
+    p.add_argument('--query-emb', default=None, type=str,
+                   help='.npy caption embedding [1,D] (output of the frozen text encoder for --input)')
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    opt = parse_args(argv)
+    os.environ.setdefault("HIP_VISIBLE_DEVICES", opt.gpu)
+    if opt.query_emb is None:
+        sys.exit("cmve inference: --query-emb is required (the frozen biGRU text encoder needs the unshipped "
+                 "student_support_set_8/model_best.pth.tar checkpoint)")
+    data = np.load(opt.gallery, allow_pickle=False)
+    scorer = GalleryScorer(data['video_embs'], [str(v) for v in data['video_ids']])
+    cap_emb = np.load(opt.query_emb, allow_pickle=False).astype(np.float32)
+    print(scorer.topk_ids(cap_emb, opt.topK))
+
+
+if __name__ == '__main__':
+    main()

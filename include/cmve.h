@@ -1,0 +1,212 @@
+/*
+ * cmve.h -- C ABI of libcmve.so, the MI355X-native (gfx950) retrieval hot path.
+ *
+ * The reference (WWWindrunner/Cross-Modal-Video-Engine) is pure Python/numpy;
+ * it has no FFI.  Each entry point below replaces a Python/numpy call site on
+ * the retrieval hot path; the replaced site is cited per function.  The Python
+ * host mirror (cross-modal-video-engine_amd/cmve) binds these with ctypes and
+ * keeps the reference's call signatures.
+ *
+ * Conventions
+ *  - every call returns int status: 0 = CMVE_OK, negative = CMVE_E_*;
+ *    cmve_last_error() returns a thread-local message for the last failure.
+ *  - all array arguments are caller-owned DEVICE pointers (HBM), unless a
+ *    parameter says "host".  No call allocates or synchronises: work is
+ *    enqueued on the handle's stream (graph-capturable).
+ *  - row-major matrices, leading dimension in ELEMENTS.
+ */
+#ifndef CMVE_H
+#define CMVE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMVE_ABI_VERSION 1
+
+enum cmve_status {
+  CMVE_OK = 0,
+  CMVE_E_INVALID = -1,   /* bad argument / shape */
+  CMVE_E_HIP = -2,       /* HIP runtime error (launch / memset) */
+  CMVE_E_UNSUPPORTED = -3,
+};
+
+enum cmve_dtype { CMVE_F32 = 0, CMVE_F64 = 1, CMVE_BF16 = 2, CMVE_I32 = 3, CMVE_I64 = 4 };
+
+/* precision of the similarity MFMA pass */
+enum cmve_sim_mode {
+  CMVE_SIM_BF16 = 0,    /* hi . hi                         (one bf16 MFMA per k-step)   */
+  CMVE_SIM_BF16X3 = 1,  /* hi.hi + hi.lo + lo.hi  (split-bf16, ~1e-6 of fp64 cosine)     */
+};
+
+/* rank directions for cmve_rank_count */
+enum cmve_rank_dir { CMVE_DIR_ROW = 1, CMVE_DIR_COL = 2 };
+
+/* Tile geometry of the packed planes: rows padded to CMVE_ROW_ALIGN,
+ * dimension padded to CMVE_DIM_ALIGN (zero fill). */
+#define CMVE_ROW_ALIGN 128
+#define CMVE_DIM_ALIGN 64
+
+/*
+ * A packed, L2-normalised embedding set resident in HBM.  Produced by
+ * cmve_pack_rows; consumed by every scoring call.  All pointers are device
+ * pointers owned by the caller (sizes from cmve_pack_size).
+ *   hi/lo   : [n_pad, d_pad] bf16 planes; x_hat ~= hi (+ lo)
+ *   raw     : the caller's un-normalised input rows (f32 or f64) -- read by
+ *             the exact fp64 fix-up; must stay alive while the set is used
+ *   inv_norm: [n_pad] fp64 1/||raw_i|| (NaN for a zero row when eps == 0)
+ *   err_hi  : [n_pad] upper bound of ||x_hat_i - hi_i||_2
+ *   err_hilo: [n_pad] upper bound of ||x_hat_i - hi_i - lo_i||_2
+ *   err_max : [2] max over rows of err_hi / err_hilo
+ */
+typedef struct cmve_rows {
+  int64_t n, d, n_pad, d_pad;
+  uint16_t* hi;
+  uint16_t* lo;
+  const void* raw;
+  int32_t raw_dtype;
+  int32_t _pad0;
+  int64_t raw_ld;
+  double* inv_norm;
+  float* err_hi;
+  float* err_hilo;
+  float* err_max;
+  double eps;            /* normalisation epsilon: 0 = LINAS l2norm, 1e-12 = F.normalize */
+} cmve_rows_t;
+
+typedef struct cmve_handle* cmve_handle_t;
+
+/* ---- handle / errors ---------------------------------------------------- */
+int cmve_abi_version(void);
+const char* cmve_last_error(void);
+int cmve_create(int device, void* hip_stream, cmve_handle_t* out);
+int cmve_set_stream(cmve_handle_t h, void* hip_stream);
+int cmve_destroy(cmve_handle_t h);
+
+/* padded sizes for a [n, d] set */
+int cmve_pack_size(int64_t n, int64_t d, int64_t* n_pad, int64_t* d_pad);
+
+/*
+ * K1 -- row L2 normalisation + split-bf16 packing of an embedding set.
+ * Replaces: LINAS-engine/evaluation.py:10-14 (l2norm), LINAS-engine/model.py:35-40
+ * (l2norm, no eps), MultiFusion/src/combiner.py:134,180 and
+ * MultiFusion/src/validate.py:55 (F.normalize, eps 1e-12).
+ * Fills rows->{hi, lo, inv_norm, err_hi, err_hilo, err_max}; rows->raw/raw_dtype/
+ * raw_ld/n/d/eps describe the input.  lo may be NULL (bf16-only set).
+ */
+int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* rows);
+
+/*
+ * K1' -- plain row normalisation y = x / max(||x||, eps)  (f32/f64 in, f32/f64 out).
+ * Replaces the same sites as cmve_pack_rows when the caller wants the normalised
+ * matrix itself (e.g. MultiFusion predicted features).
+ */
+int cmve_l2norm_rows(cmve_handle_t h, const void* x, int32_t x_dtype, int64_t ldx,
+                     void* y, int32_t y_dtype, int64_t ldy, int64_t n, int64_t d, double eps);
+
+/*
+ * K4(a) -- similarity GEMM with store epilogue: out[i, j] = alpha * (q_i . g_j) + beta
+ * for i < q->n, j < g->n.  bf16 / split-bf16 MFMA, LDS-staged 128x128x64 tiles.
+ * Replaces: LINAS-engine/evaluation.py:21 (-1 * np.dot -> alpha=-1),
+ * LINAS-engine/evaluation.py:83 (cal_simi, alpha=1), LINAS-engine/loss.py:10
+ * (cosine_sim), MultiFusion/src/validate.py:73,90 and MultiFusion/src/inference.py:63
+ * (1 - pred @ index.T -> alpha=-1, beta=1), MultiFusion/src/combiner.py:136 (alpha=100).
+ * out_dtype: CMVE_F32 or CMVE_F64.
+ */
+int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode,
+                   float alpha, float beta, void* out, int32_t out_dtype, int64_t ldo);
+
+/*
+ * K5a -- exact fp64 GT scores and rank thresholds for one direction.
+ * For every row a of `a_set` with GT list idx[off[a] .. off[a+1]) into `b_set`:
+ *   sgt[a]    = max_k cos64(a, b_k)          (NaN if the list is empty)
+ *   thr_hi[a] = fp32 round-up  (sgt + E_a),  thr_lo[a] = fp32 round-down (sgt - E_a)
+ * E_a is the rigorous error bound of the `mode` MFMA score.
+ * Rows with no GT or padding get thr = +inf (never counted).  Arrays sized a_set->n_pad.
+ * Replaces the GT lookup in LINAS-engine/util/metrics.py:140-147.
+ */
+int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a_set, const cmve_rows_t* b_set,
+                       int32_t mode, const int64_t* off, const int32_t* idx,
+                       double* sgt, float* thr_hi, float* thr_lo);
+
+/*
+ * K4(b)+K5 -- fused score -> rank count, both directions in ONE GEMM pass, the
+ * score matrix is never materialised:
+ *   row_cnt[i] = #{ j : cos64(q_i, g_j) > row_sgt[i] }   (if CMVE_DIR_ROW in dirs)
+ *   col_cnt[j] = #{ i : cos64(q_i, g_j) > col_sgt[j] }   (if CMVE_DIR_COL in dirs)
+ * The MFMA pass counts the pairs that are certain under the error bound and
+ * appends the undecided (i, j) pairs to `cand` (capacity cand_cap, uint64 each);
+ * an fp64 fix-up kernel re-scores those exactly.  *cand_count (device int64)
+ * receives the number of undecided pairs; if it exceeds cand_cap the counts are
+ * incomplete and the caller must retry with a larger buffer.
+ * gt rank (1-based) = 1 + cnt, i.e. the position of the best GT in the reference's
+ * np.argsort (LINAS-engine/util/metrics.py:137-147) on tie-free inputs.
+ * row_cnt/col_cnt are zeroed by the call.
+ */
+int cmve_rank_count(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode,
+                    int32_t dirs,
+                    const double* row_sgt, const float* row_hi, const float* row_lo,
+                    const double* col_sgt, const float* col_hi, const float* col_lo,
+                    int32_t* row_cnt, int32_t* col_cnt,
+                    uint64_t* cand, int64_t cand_cap, int64_t* cand_count);
+
+/* The two halves of cmve_rank_count, for callers that time or overlap them separately:
+ * the MFMA pass (zeroes the counters, counts certain pairs, appends undecided ones) ... */
+int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs,
+                   const float* row_hi, const float* row_lo, const float* col_hi, const float* col_lo,
+                   int32_t* row_cnt, int32_t* col_cnt, uint64_t* cand, int64_t cand_cap, int64_t* cand_count);
+/* ... and the exact fp64 re-score of the undecided pairs. */
+int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
+                    const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
+                    const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count);
+
+/*
+ * Thresholds from GIVEN exact GT scores sgt[a_set->n] (NaN = no GT): the sharded path,
+ * where the owner rank of a query's GT computes sgt and all-gathers it with the query.
+ * thr_hi/thr_lo as cmve_gt_thresholds, against the error bound of `b_set` (the local shard).
+ */
+int cmve_rank_thresholds(cmve_handle_t h, const cmve_rows_t* a_set, const cmve_rows_t* b_set, int32_t mode,
+                         const double* sgt, float* thr_hi, float* thr_lo);
+
+/*
+ * Rank from a given score matrix (no GEMM): for each row i of errors[n_q, n_m]
+ * (f32 or f64, lower = better, as LINAS errors), with GT lists off/idx:
+ *   cnt[i] = #{ j : e_ij < min_{k in GT(i)} e_ik }   (0 if GT(i) is empty: the caller
+ *   maps empty lists to rank n_m + 1, as metrics.py:140 initialises it).
+ * transposed != 0 ranks the columns of `errors` instead (errors.T rows).
+ * Replaces: LINAS-engine/util/metrics.py:124-147 (eval_q2m's argsort loop).
+ */
+int cmve_rank_from_matrix(cmve_handle_t h, const void* errors, int32_t dtype, int64_t n_rows,
+                          int64_t n_cols, int64_t ld, int32_t transposed,
+                          const int64_t* off, const int32_t* idx, int32_t* cnt);
+
+/*
+ * Positions of every GT item in a given error matrix (mAP, LINAS-engine/util/metrics.py:61-102):
+ *   pos[k] = #{ j : e_ij < e_{i, idx[k]} }   for every k in [off[i], off[i+1])
+ * (position in np.argsort = pos + 1 on tie-free rows; a NaN GT gets n_cols / n_rows).
+ * transposed != 0 ranks the columns of `errors` (errors.T rows).  pos is int32 [off[n]].
+ */
+int cmve_gt_positions_from_matrix(cmve_handle_t h, const void* errors, int32_t dtype, int64_t n_rows,
+                                  int64_t n_cols, int64_t ld, int32_t transposed,
+                                  const int64_t* off, const int32_t* idx, int32_t* pos);
+
+/*
+ * K4(c) -- exact top-k per query (LINAS-engine/inference.py:78-79:
+ * np.argsort(errors[0])[:topK]).  The MFMA pass writes approximate scores into
+ * `scores_ws` [q->n_pad, g->n_pad] fp32; one block per query radix-selects the
+ * k-th score and keeps every column within 2E of it (E = rigorous score error
+ * bound; at most 4096 per query), re-scores them in fp64 and sorts them
+ * (score desc, index asc).  out_idx [q->n, k] int32, out_score [q->n, k] fp64
+ * (the exact cosine).  *overflow (device int32) becomes non-zero if a query kept
+ * more than 4096 columns (retry with CMVE_SIM_BF16X3, whose band is ~10x narrower).
+ * 1 <= k <= 2048.
+ */
+int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
+              float* scores_ws, int32_t* out_idx, double* out_score, int32_t* overflow);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMVE_H */

@@ -1,0 +1,52 @@
+"""The C ABI library builds for gfx950, loads, and exports every symbol include/cmve.h declares.
+
+CPU-only: no kernel is launched here (host-only entry points only)."""
+import ctypes as C
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cmve.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cmve_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_the_hot_path():
+    names = declared_functions()
+    for must in ("cmve_pack_rows", "cmve_sim_store", "cmve_gt_thresholds", "cmve_rank_count",
+                 "cmve_rank_from_matrix", "cmve_gt_positions_from_matrix", "cmve_topk"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from cmve import _lib
+    for name in declared_functions():
+        assert hasattr(_lib.lib, name), f"{name} declared in cmve.h but not exported"
+    assert set(declared_functions()) <= set(_lib.exported_symbols())
+
+
+def test_host_only_entry_points():
+    from cmve import _lib
+    assert _lib.lib.cmve_abi_version() == 1
+    n_pad, d_pad = C.c_int64(), C.c_int64()
+    assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
+    assert (n_pad.value, d_pad.value) == (1024, 1024)
+    assert _lib.lib.cmve_pack_size(1, 100, C.byref(n_pad), C.byref(d_pad)) == 0
+    assert (n_pad.value, d_pad.value) == (128, 128)
+    assert _lib.lib.cmve_pack_size(-1, 100, C.byref(n_pad), C.byref(d_pad)) < 0
+    assert b"pack_size" in _lib.lib.cmve_last_error()
+
+
+def test_rows_struct_layout_matches_header():
+    from cmve import _lib
+    # 4 int64 + 2 ptr + ptr + 2 int32 + int64 + 4 ptr + double = 13 * 8 bytes
+    assert C.sizeof(_lib.Rows) == 8 * 4 + 8 * 2 + 8 + 4 * 2 + 8 + 8 * 4 + 8
+
+
+def test_gfx950_code_object_present():
+    from cmve import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
