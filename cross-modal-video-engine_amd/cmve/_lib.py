@@ -20,7 +20,7 @@ lib = C.CDLL(LIB_PATH)
 # ---- enums (include/cmve.h) ----
 CMVE_OK = 0
 CMVE_F32, CMVE_F64, CMVE_BF16, CMVE_I32, CMVE_I64 = 0, 1, 2, 3, 4
-SIM_BF16, SIM_BF16X3 = 0, 1
+SIM_BF16, SIM_BF16X3, SIM_F16 = 0, 1, 2
 DIR_ROW, DIR_COL = 1, 2
 ROW_ALIGN, DIM_ALIGN = 128, 64
 TOPK_MAX = 2048
@@ -34,6 +34,7 @@ class Rows(C.Structure):
         ("raw", C.c_void_p), ("raw_dtype", C.c_int32), ("_pad0", C.c_int32), ("raw_ld", C.c_int64),
         ("inv_norm", C.c_void_p), ("err_hi", C.c_void_p), ("err_hilo", C.c_void_p), ("err_max", C.c_void_p),
         ("eps", C.c_double),
+        ("h16", C.c_void_p), ("err_h16", C.c_void_p),
     ]
 
 
@@ -46,6 +47,7 @@ SIGNATURES = {
     "cmve_create": (C.c_int, [C.c_int, _vp, _P(_vp)]),
     "cmve_set_stream": (C.c_int, [_vp, _vp]),
     "cmve_destroy": (C.c_int, [_vp]),
+    "cmve_mfma_probe": (C.c_int, [_vp, _vp]),
     "cmve_pack_size": (C.c_int, [_i64, _i64, _P(_i64), _P(_i64)]),
     "cmve_pack_rows": (C.c_int, [_vp, _P(Rows)]),
     "cmve_l2norm_rows": (C.c_int, [_vp, _vp, _i32, _i64, _vp, _i32, _i64, _i64, _i64, _f64]),
@@ -67,8 +69,9 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-if lib.cmve_abi_version() != 1:
-    raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != 1")
+ABI_VERSION = 2
+if lib.cmve_abi_version() != ABI_VERSION:
+    raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 
 
 class CmveError(RuntimeError):

@@ -36,13 +36,68 @@ def shard_bounds(n_global: int, world: int, rank: int):
     return lo, min(n_global, lo + per)
 
 
+# ---- collective steps (device-agnostic: RCCL on the GPU path, gloo in the CPU tests) ----
+
+def local_gt_lists(gts_global: Sequence[Sequence[int]], lo: int, hi: int):
+    """GT lists restricted to the shard [lo, hi), re-indexed locally."""
+    return [[g - lo for g in l if lo <= g < hi] for l in gts_global]
+
+
+def merge_gt_scores(sgt_partial: torch.Tensor, world: int) -> torch.Tensor:
+    """all-reduce(MAX) of per-shard best-GT scores; NaN (no GT in this shard) -> -inf -> NaN."""
+    if world == 1:
+        return sgt_partial
+    s = torch.nan_to_num(sgt_partial, nan=-np.inf)
+    dist.all_reduce(s, op=dist.ReduceOp.MAX)
+    return torch.where(torch.isinf(s) & (s < 0), torch.full_like(s, float('nan')), s)
+
+
+def reduce_counts(cnt: torch.Tensor, world: int) -> torch.Tensor:
+    """all-reduce(SUM) of per-shard better-than-GT counts."""
+    if world > 1:
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    return cnt
+
+
+def ranks_from(cnt: torch.Tensor, sgt: torch.Tensor, n_q: int, n_global: int) -> torch.Tensor:
+    no_gt = torch.isnan(sgt[:n_q])
+    c = cnt[:n_q].to(torch.int64)
+    return torch.where(no_gt, torch.full_like(c, n_global + 1), c + 1)
+
+
+def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: int):
+    """Gather every shard's local top-k (global ids, fp64 scores) and keep the best k per query,
+    ordered (score desc, global id asc).  idx_global/scores: [n_q, k_local]."""
+    n_q, kk = idx_global.shape
+    if world > 1:
+        gi = torch.empty((world * n_q, kk), dtype=idx_global.dtype, device=idx_global.device)
+        gs = torch.empty((world * n_q, kk), dtype=scores.dtype, device=scores.device)
+        dist.all_gather_into_tensor(gi, idx_global.contiguous())
+        dist.all_gather_into_tensor(gs, scores.contiguous())
+        idx_global = gi.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
+        scores = gs.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
+    idx_h = idx_global.cpu().numpy()
+    sc_h = scores.cpu().numpy()
+    kout = min(k, idx_h.shape[1])
+    out = np.empty((n_q, kout), np.int64)
+    out_s = np.empty((n_q, kout))
+    for i in range(n_q):
+        valid = idx_h[i] >= 0
+        order = np.lexsort((idx_h[i][valid], -sc_h[i][valid]))[:kout]
+        out[i, :order.size] = idx_h[i][valid][order]
+        out_s[i, :order.size] = sc_h[i][valid][order]
+        out[i, order.size:] = -1
+        out_s[i, order.size:] = np.nan
+    return out, out_s
+
+
 class ShardedGallery:
     """This rank's gallery shard, packed in HBM, plus the global row offset."""
 
     def __init__(self, local_embs, offset: int, n_global: int, with_lo: bool = False, eps: float = 0.0,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, with_f16: bool = True):
         self.rank, self.world = _world()
-        self.shard = engine.RowSet(local_embs, eps=eps, with_lo=with_lo, device=device)
+        self.shard = engine.RowSet(local_embs, eps=eps, with_lo=with_lo, device=device, with_f16=with_f16)
         self.device = self.shard.device
         self.offset = int(offset)
         self.n_global = int(n_global)
@@ -51,9 +106,7 @@ class ShardedGallery:
 
     # ---- GT lists restricted to this shard ----
     def local_gt_csr(self, gts_global: Sequence[Sequence[int]]):
-        lo, hi = self.offset, self.offset + self.shard.n
-        local = [[g - lo for g in l if lo <= g < hi] for l in gts_global]
-        return engine.csr(local, self.device)
+        return engine.csr(local_gt_lists(gts_global, self.offset, self.offset + self.shard.n), self.device)
 
     def all_gather_rows(self, x_local: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -63,26 +116,22 @@ class ShardedGallery:
         dist.all_gather_into_tensor(out, x_local.contiguous())
         return out
 
-    def rank_queries(self, q_local: torch.Tensor, gt_csr, n_q: int, mode: int = _lib.SIM_BF16, events=None,
+    def rank_queries(self, q_local: torch.Tensor, gt_csr, n_q: int, mode: int = _lib.SIM_F16, events=None,
                      return_host: bool = True):
         """Global 1-based GT ranks of all gathered queries (t2v direction).
 
         q_local: this rank's [n_local, D] query embeddings (equal n_local on every rank);
         gt_csr: (off, idx) from ``local_gt_csr`` for the GATHERED query order."""
         q_all = self.all_gather_rows(q_local)
-        q = engine.RowSet(q_all, with_lo=(mode == _lib.SIM_BF16X3), device=self.device)
+        q = engine.RowSet(q_all, with_lo=(mode == _lib.SIM_BF16X3), with_f16=(mode == _lib.SIM_F16),
+                          device=self.device)
         off, idx = gt_csr
         sgt, _, _ = engine.gt_thresholds(q, self.shard, off, idx, mode)
-        if self.world > 1:
-            sgt = torch.nan_to_num(sgt, nan=-np.inf)
-            dist.all_reduce(sgt, op=dist.ReduceOp.MAX)
-            sgt = torch.where(torch.isinf(sgt) & (sgt < 0), torch.full_like(sgt, float('nan')), sgt)
+        sgt = merge_gt_scores(sgt, self.world)
         hi, lo = engine.rank_thresholds(q, self.shard, sgt, mode)
         cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events)
-        if self.world > 1:
-            dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        no_gt = torch.isnan(sgt[:n_q])
-        ranks = torch.where(no_gt, torch.full_like(cnt[:n_q], self.n_global + 1), cnt[:n_q] + 1)
+        cnt = reduce_counts(cnt, self.world)
+        ranks = ranks_from(cnt, sgt, n_q, self.n_global)
         if not return_host:
             return ranks
         ncand = int(self.ws.count.item())
@@ -91,28 +140,15 @@ class ShardedGallery:
             return self.rank_queries(q_local, gt_csr, n_q, mode, None, return_host)
         return ranks.cpu().numpy().astype(np.int64)
 
-    def topk(self, q_local: torch.Tensor, k: int, mode: int = _lib.SIM_BF16):
+    def topk(self, q_local: torch.Tensor, k: int, mode: int = _lib.SIM_F16):
         """Global exact top-k (global ids, fp64 cosines) of all gathered queries."""
         q_all = self.all_gather_rows(q_local)
-        q = engine.RowSet(q_all, with_lo=self.shard.has_lo, device=self.device)
+        q = engine.RowSet(q_all, with_lo=self.shard.has_lo, with_f16=self.shard.has_f16, device=self.device)
         kk = min(k, self.shard.n)
         idx, sc = engine.topk(q, self.shard, kk, mode=mode)
-        idx = torch.from_numpy(idx + self.offset).to(self.device)
+        idx = torch.from_numpy(np.where(idx >= 0, idx + self.offset, -1)).to(self.device)
         sc = torch.from_numpy(sc).to(self.device)
-        if self.world > 1:
-            idx = self.all_gather_rows(idx.unsqueeze(0).contiguous()).reshape(self.world, q.n, kk)
-            sc = self.all_gather_rows(sc.unsqueeze(0).contiguous()).reshape(self.world, q.n, kk)
-            idx = idx.permute(1, 0, 2).reshape(q.n, -1)
-            sc = sc.permute(1, 0, 2).reshape(q.n, -1)
-        idx_h = idx.cpu().numpy()
-        sc_h = sc.cpu().numpy()
-        out = np.empty((q.n, min(k, idx_h.shape[1])), np.int64)
-        out_s = np.empty(out.shape)
-        for i in range(q.n):
-            order = np.lexsort((idx_h[i], -sc_h[i]))[:out.shape[1]]  # score desc, global id asc
-            out[i] = idx_h[i, order]
-            out_s[i] = sc_h[i, order]
-        return out, out_s
+        return merge_topk(idx, sc, k, self.world)
 
 
 def metrics_from_ranks(ranks: np.ndarray) -> List[float]:

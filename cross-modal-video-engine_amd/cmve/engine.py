@@ -85,7 +85,8 @@ class RowSet:
     The raw rows are kept: the exact fp64 fix-up reads them.
     """
 
-    def __init__(self, x, eps: float = 0.0, with_lo: bool = True, device: Optional[torch.device] = None):
+    def __init__(self, x, eps: float = 0.0, with_lo: bool = True, device: Optional[torch.device] = None,
+                 with_f16: bool = True):
         device = device or default_device()
         raw = to_device(x, device)
         if raw.dim() != 2:
@@ -103,18 +104,26 @@ class RowSet:
         self.inv_norm = torch.empty(n_pad, dtype=torch.float64, device=device)
         self.err_hi = torch.empty(n_pad, dtype=torch.float32, device=device)
         self.err_hilo = torch.empty(n_pad, dtype=torch.float32, device=device)
-        self.err_max = torch.empty(2, dtype=torch.float32, device=device)
+        self.h16 = torch.empty((n_pad, d_pad), dtype=torch.int16, device=device) if with_f16 else None
+        self.err_h16 = torch.empty(n_pad, dtype=torch.float32, device=device) if with_f16 else None
+        self.err_max = torch.empty(3, dtype=torch.float32, device=device)
         self.desc = Rows(n=n, d=d, n_pad=n_pad, d_pad=d_pad, hi=self.hi.data_ptr(),
                          lo=self.lo.data_ptr() if self.lo is not None else None,
                          raw=raw.data_ptr() if n else None, raw_dtype=_dtype_code(raw), _pad0=0,
                          raw_ld=raw.stride(0) if n else d, inv_norm=self.inv_norm.data_ptr(),
                          err_hi=self.err_hi.data_ptr(), err_hilo=self.err_hilo.data_ptr(),
-                         err_max=self.err_max.data_ptr(), eps=self.eps)
+                         err_max=self.err_max.data_ptr(), eps=self.eps,
+                         h16=self.h16.data_ptr() if with_f16 else None,
+                         err_h16=self.err_h16.data_ptr() if with_f16 else None)
         check(lib.cmve_pack_rows(handle(device), C.byref(self.desc)), "cmve_pack_rows")
 
     @property
     def has_lo(self):
         return self.lo is not None
+
+    @property
+    def has_f16(self):
+        return self.h16 is not None
 
     def normalized(self, dtype=torch.float64) -> torch.Tensor:
         """x / max(||x||, eps) on device (K1')."""
@@ -216,7 +225,7 @@ def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: O
     return row_cnt, col_cnt
 
 
-def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int = _lib.SIM_BF16,
+def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int = _lib.SIM_F16,
                    ws: Optional[RankWorkspace] = None):
     """Exact GT ranks in both directions from ONE fused GEMM pass.
 
@@ -228,6 +237,8 @@ def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int =
         raise ValueError("gt_rank_counts: need row_gts and/or col_gts")
     if mode == _lib.SIM_BF16X3 and not (q.has_lo and g.has_lo):
         raise ValueError("BF16X3 needs lo planes")
+    if mode == _lib.SIM_F16 and not (q.has_f16 and g.has_f16):
+        mode = _lib.SIM_BF16
     ws = ws or RankWorkspace(q.device, cap=max(1 << 16, 64 * (q.n + g.n)))
     row = col = None
     if row_gts is not None:
@@ -275,7 +286,7 @@ def rank_from_matrix(errors, gts, transposed: bool = False, device=None) -> np.n
     return ranks
 
 
-def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_BF16, scores_ws: Optional[torch.Tensor] = None):
+def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Optional[torch.Tensor] = None):
     """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines."""
     k = int(min(k, g.n))
     if k < 1:
@@ -287,7 +298,9 @@ def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_BF16, scores_ws: Opt
     idx = torch.empty((max(q.n, 1), k), dtype=torch.int32, device=q.device)
     sc = torch.empty((max(q.n, 1), k), dtype=torch.float64, device=q.device)
     ovf = torch.zeros(1, dtype=torch.int32, device=q.device)
-    for m in ((mode, _lib.SIM_BF16X3) if (mode == _lib.SIM_BF16 and q.has_lo and g.has_lo) else (mode,)):
+    if mode == _lib.SIM_F16 and not (q.has_f16 and g.has_f16):
+        mode = _lib.SIM_BF16
+    for m in ((mode, _lib.SIM_BF16X3) if (mode != _lib.SIM_BF16X3 and q.has_lo and g.has_lo) else (mode,)):
         check(lib.cmve_topk(handle(q.device), C.byref(q.desc), C.byref(g.desc), m, k, _ptr(scores_ws), _ptr(idx),
                             _ptr(sc), _ptr(ovf)), "cmve_topk")
         if int(ovf.item()) == 0:
@@ -297,7 +310,7 @@ def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_BF16, scores_ws: Opt
     return idx[:q.n].to(torch.int64).cpu().numpy(), sc[:q.n].cpu().numpy()
 
 
-def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_BF16):
+def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
     """Exact 1-based position of EVERY GT item: for row i of `a` and k in lists[i],
     1 + #{j : cos64(a_i, b_j) > cos64(a_i, b_k)}.  Implemented as a fused rank count
     over an expanded query set (row i repeated once per GT item, GT list [k])."""
@@ -307,7 +320,7 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_BF16):
     if owners.size == 0:
         return out
     sel = torch.from_numpy(owners).to(a.device)
-    expanded = RowSet(a.raw.index_select(0, sel), eps=a.eps, with_lo=a.has_lo, device=a.device)
+    expanded = RowSet(a.raw.index_select(0, sel), eps=a.eps, with_lo=a.has_lo, device=a.device, with_f16=a.has_f16)
     r, _, _ = gt_rank_counts(expanded, b, row_gts=items, mode=mode)
     p = 0
     for i, l in enumerate(lists):

@@ -27,7 +27,7 @@ import sys
 import numpy as np
 
 from .. import engine
-from .._lib import SIM_BF16
+from .._lib import SIM_F16
 
 
 class GalleryScorer:
@@ -46,7 +46,7 @@ class GalleryScorer:
         if self._ws is None or self._ws.numel() < need:
             import torch
             self._ws = torch.empty(need, dtype=torch.float32, device=self.gallery.device)
-        idx, _ = engine.topk(q, self.gallery, topK, mode=SIM_BF16, scores_ws=self._ws)
+        idx, _ = engine.topk(q, self.gallery, topK, mode=SIM_F16, scores_ws=self._ws)
         return idx
 
     def topk_ids(self, cap_emb, topK=10):

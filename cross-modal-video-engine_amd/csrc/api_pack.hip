@@ -38,22 +38,26 @@ template <typename T>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ raw, int64_t ld, int64_t n,
                                                         int64_t d, int64_t n_pad, int64_t d_pad, double eps,
                                                         uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
-                                                        double* __restrict__ inv_norm, float* __restrict__ err_hi,
-                                                        float* __restrict__ err_hilo, float* __restrict__ err_max) {
+                                                        uint16_t* __restrict__ h16, double* __restrict__ inv_norm,
+                                                        float* __restrict__ err_hi, float* __restrict__ err_hilo,
+                                                        float* __restrict__ err_h16, float* __restrict__ err_max) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_pad) return;
   uint16_t* hrow = hi + row * d_pad;
   uint16_t* lrow = lo ? lo + row * d_pad : nullptr;
+  uint16_t* frow = h16 ? h16 + row * d_pad : nullptr;
   if (row >= n) {  // padding rows: zero vectors, zero bounds
     for (int64_t k = lane; k < d_pad; k += 64) {
       hrow[k] = 0;
       if (lrow) lrow[k] = 0;
+      if (frow) frow[k] = 0;
     }
     if (lane == 0) {
       inv_norm[row] = 0.0;
       err_hi[row] = 0.f;
       err_hilo[row] = 0.f;
+      if (err_h16) err_h16[row] = 0.f;
     }
     return;
   }
@@ -67,10 +71,16 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
   const double nrm = sqrt(ss);
   // eps == 0: LINAS l2norm (X / norm, NaN on a zero row); eps > 0: F.normalize
   const double inv = eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm;
-  double e1 = 0.0, e2 = 0.0;
+  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
   for (int64_t k = lane; k < d_pad; k += 64) {
     if (k < d) {
       const double xh = (double)x[k] * inv;
+      if (frow) {
+        const _Float16 hf16 = (_Float16)xh;  // RNE from fp64
+        const double r3 = xh - (double)hf16;
+        e3 = fma(r3, r3, e3);
+        frow[k] = __builtin_bit_cast(uint16_t, hf16);
+      }
       const float xf = (float)xh;
       const uint16_t h = f2bf(xf);
       const float hf = bf2f(h);
@@ -84,10 +94,12 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
     } else {
       hrow[k] = 0;
       if (lrow) lrow[k] = 0;
+      if (frow) frow[k] = 0;
     }
   }
   e1 = wave_sum(e1);
   e2 = wave_sum(e2);
+  e3 = wave_sum(e3);
   if (lane == 0) {
     inv_norm[row] = inv;
     // sqrt rounding + the fp64 error of x*inv itself (~1e-16 per element) -> small slack
@@ -97,6 +109,11 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
     err_hilo[row] = b2;
     if (b1 == b1) atomicMax((int*)&err_max[0], __float_as_int(b1));  // non-negative floats order as ints
     if (b2 == b2) atomicMax((int*)&err_max[1], __float_as_int(b2));
+    if (err_h16) {
+      const float b3 = f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12);
+      err_h16[row] = b3;
+      if (b3 == b3) atomicMax((int*)&err_max[2], __float_as_int(b3));
+    }
   }
 }
 
@@ -172,16 +189,17 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
   CMVE_REQUIRE(r->n == 0 || r->raw, "cmve_pack_rows: raw is NULL");
   CMVE_REQUIRE(r->raw_ld >= r->d, "cmve_pack_rows: raw_ld < d");
   CMVE_REQUIRE(r->eps >= 0.0, "cmve_pack_rows: eps < 0");
-  CMVE_HIP(hipMemsetAsync(r->err_max, 0, 2 * sizeof(float), h->stream));
+  CMVE_REQUIRE((r->h16 == nullptr) == (r->err_h16 == nullptr), "cmve_pack_rows: h16 and err_h16 go together");
+  CMVE_HIP(hipMemsetAsync(r->err_max, 0, 3 * sizeof(float), h->stream));
   dim3 grid((unsigned)((r->n_pad + 3) / 4)), block(256);
   if (r->raw_dtype == CMVE_F32)
     hipLaunchKernelGGL(pack_rows_kernel<float>, grid, block, 0, h->stream, (const float*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->inv_norm, r->err_hi, r->err_hilo,
-                       r->err_max);
+                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
+                       r->err_h16, r->err_max);
   else if (r->raw_dtype == CMVE_F64)
     hipLaunchKernelGGL(pack_rows_kernel<double>, grid, block, 0, h->stream, (const double*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->inv_norm, r->err_hi, r->err_hilo,
-                       r->err_max);
+                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
+                       r->err_h16, r->err_max);
   else {
     set_error("cmve_pack_rows: raw_dtype must be CMVE_F32 or CMVE_F64");
     return CMVE_E_INVALID;

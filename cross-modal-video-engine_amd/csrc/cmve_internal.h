@@ -86,14 +86,24 @@ __device__ __forceinline__ float f32_round_down(double x) {
   return f;
 }
 
-// Rigorous bound on |score_mfma(i,j) - cos_exact(i,j)| for row errors ea, eb (see DESIGN.md s4):
-//   representation:  ea + (1 + ea) * eb
-//   accumulation:    gamma_n * (1 + ea) * (1 + eb), n = roundings along the fp32 chain
+// Rigorous bound on |score_mfma(i,j) - cos_exact(i,j)| for row errors ea, eb (DESIGN.md s4):
+//   representation:  ea + (1 + ea) * eb          (Cauchy-Schwarz on x_hat - x_tilde)
+//   accumulation:    gamma_n * (1 + ea) * (1 + eb)
+// n counts roundings as if every product and the C operand of each 32-deep
+// v_mfma_f32_16x16x32 were added with its own rounding (33 per 32 products), at
+// u = 2^-23 (2x RNE: covers the truncating alignment the MFMA probe shows -- it drops
+// product bits below ~2^-24 of the largest term, tests/test_gpu_numerics.py).
 __host__ __device__ __forceinline__ double score_error_bound(double ea, double eb, int64_t d_pad, int mode) {
-  const double n = (double)d_pad * (mode == CMVE_SIM_BF16X3 ? 3.0 : 1.0);
-  const double u = 1.0 / 8388608.0;  // 2^-23 (2x the RNE unit roundoff: covers truncating adders)
+  const double n = (double)d_pad * (33.0 / 32.0) * (mode == CMVE_SIM_BF16X3 ? 3.0 : 1.0);
+  const double u = 1.0 / 8388608.0;  // 2^-23
   const double gamma = n * u / (1.0 - n * u);
   return ea + (1.0 + ea) * eb + gamma * (1.0 + ea) * (1.0 + eb) + 1e-12;
 }
+
+// per-row error plane and err_max slot of a sim mode (err_max = {hi, hilo, h16})
+inline const float* mode_err(const cmve_rows_t* r, int mode) {
+  return mode == CMVE_SIM_BF16 ? r->err_hi : (mode == CMVE_SIM_BF16X3 ? r->err_hilo : r->err_h16);
+}
+__host__ __device__ __forceinline__ int mode_slot(int mode) { return mode; }
 
 }  // namespace cmve

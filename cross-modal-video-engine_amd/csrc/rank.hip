@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void gt_thr_kernel(const TA* __restrict__ araw
       thr_hi[row] = INFINITY;
       thr_lo[row] = INFINITY;
     } else {
-      const double E = score_error_bound((double)aerr[row], (double)berr_max[mode == CMVE_SIM_BF16 ? 0 : 1], d_pad,
+      const double E = score_error_bound((double)aerr[row], (double)berr_max[mode_slot(mode)], d_pad,
                                          mode);
       sgt[row] = best;
       thr_hi[row] = f32_round_up(best + E);
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void thr_from_sgt_kernel(const double* __restr
     thr_lo[row] = INFINITY;
     return;
   }
-  const double E = score_error_bound((double)aerr[row], (double)berr_max[mode == CMVE_SIM_BF16 ? 0 : 1], d_pad, mode);
+  const double E = score_error_bound((double)aerr[row], (double)berr_max[mode_slot(mode)], d_pad, mode);
   thr_hi[row] = f32_round_up(s + E);
   thr_lo[row] = f32_round_down(s - E);
 }
@@ -278,10 +278,12 @@ extern "C" int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a, const c
                                   float* thr_lo) {
   CMVE_REQUIRE(h && a && b, "cmve_gt_thresholds: NULL argument");
   CMVE_REQUIRE(a->d == b->d && a->d_pad == b->d_pad, "cmve_gt_thresholds: dimension mismatch");
-  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3, "cmve_gt_thresholds: unknown mode");
+  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
+               "cmve_gt_thresholds: unknown mode");
   CMVE_REQUIRE(off && sgt && thr_hi && thr_lo, "cmve_gt_thresholds: NULL output");
   CMVE_REQUIRE(a->n == 0 || (a->raw && b->raw && idx), "cmve_gt_thresholds: raw rows / idx missing");
-  const float* aerr = mode == CMVE_SIM_BF16 ? a->err_hi : a->err_hilo;
+  const float* aerr = mode_err(a, mode);
+  CMVE_REQUIRE(aerr, "cmve_gt_thresholds: set has no error plane for this mode");
   dim3 grid((unsigned)((a->n_pad + 3) / 4)), block(256);
 #define GT(TA, TB)                                                                                                   \
   hipLaunchKernelGGL((gt_thr_kernel<TA, TB>), grid, block, 0, h->stream, (const TA*)a->raw, a->raw_ld, a->inv_norm, \
@@ -354,8 +356,10 @@ extern "C" int cmve_rank_thresholds(cmve_handle_t h, const cmve_rows_t* a, const
                                     const double* sgt, float* thr_hi, float* thr_lo) {
   CMVE_REQUIRE(h && a && b && sgt && thr_hi && thr_lo, "cmve_rank_thresholds: NULL argument");
   CMVE_REQUIRE(a->d_pad == b->d_pad, "cmve_rank_thresholds: dimension mismatch");
-  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3, "cmve_rank_thresholds: unknown mode");
-  const float* aerr = mode == CMVE_SIM_BF16 ? a->err_hi : a->err_hilo;
+  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
+               "cmve_rank_thresholds: unknown mode");
+  const float* aerr = mode_err(a, mode);
+  CMVE_REQUIRE(aerr, "cmve_rank_thresholds: set has no error plane for this mode");
   hipLaunchKernelGGL(thr_from_sgt_kernel, dim3((unsigned)((a->n_pad + 255) / 256)), dim3(256), 0, h->stream, sgt, aerr,
                      a->n, a->n_pad, b->err_max, a->d_pad, mode, thr_hi, thr_lo);
   return check_launch("thr_from_sgt_kernel");

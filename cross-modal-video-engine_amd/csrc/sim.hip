@@ -17,6 +17,7 @@
 namespace cmve {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -24,6 +25,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int PLANE_BYTES = BM * BK * 2;  // 16 KiB
 constexpr int EPI_STORE = 0, EPI_RANK = 1;
+constexpr int CAND_LDS = 1024;  // per-block undecided-pair buffer (one global atomic per block)
 
 struct SimArgs {
   const uint16_t* qhi;
@@ -78,10 +80,19 @@ __device__ __forceinline__ void stage_plane(const uint16_t* __restrict__ src, in
   }
 }
 
-__device__ __forceinline__ bf16x8_t read_frag(const char* plane, int row, int chunk) {
+__device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chunk) {
   // row & 7 == lane & 7 for every fragment row this kernel reads
-  const s16x8_t v = *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
-  return __builtin_bit_cast(bf16x8_t, v);
+  return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
+}
+
+template <int MODE>
+__device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
+  if constexpr (MODE == CMVE_SIM_F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
 }
 
 template <int MODE, int EPI>
@@ -98,7 +109,12 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
 
   int* lds_rc = (int*)(smem + 2 * STAGE_BYTES);
   int* lds_cc = lds_rc + BM;
-  if (EPI == EPI_RANK) lds_rc[tid] = 0;  // 256 ints: 128 row + 128 col counters
+  unsigned long long* lds_cand = (unsigned long long*)(lds_cc + BN);
+  unsigned* lds_ncand = (unsigned*)(lds_cand + CAND_LDS);
+  if (EPI == EPI_RANK) {
+    lds_rc[tid] = 0;  // 256 ints: 128 row + 128 col counters
+    if (tid == 0) *lds_ncand = 0u;
+  }
 
   auto stage = [&](int t, int s) {
     char* base = smem + s * STAGE_BYTES;
@@ -130,7 +146,7 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
-      bf16x8_t fa[4], fb[4];
+      s16x8_t fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = read_frag(pA, wr * 64 + i * 16 + frow, chunk);
 #pragma unroll
@@ -138,7 +154,7 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
       if (MODE == CMVE_SIM_BF16X3) {
         const char* pAl = base + 2 * PLANE_BYTES;
         const char* pBl = base + 3 * PLANE_BYTES;
-        bf16x8_t la[4], lb[4];
+        s16x8_t la[4], lb[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) la[i] = read_frag(pAl, wr * 64 + i * 16 + frow, chunk);
 #pragma unroll
@@ -147,15 +163,15 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[i], fb[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], lb[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma<MODE>(la[i], fb[j], acc[i][j]);
+            acc[i][j] = mfma<MODE>(fa[i], lb[j], acc[i][j]);
           }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma<MODE>(fa[i], fb[j], acc[i][j]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -222,10 +238,15 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
           cc_pack += (uint32_t)bc << (8 * j);
           const uint32_t flags = (uint32_t)((s >= rlo[i][r]) & !br) | ((uint32_t)((s >= clo[j]) & !bc) << 1);
           if (flags) {
-            const unsigned long long slot = atomicAdd(a.cand_count, 1ull);
-            if ((long long)slot < a.cand_cap)
-              a.cand[slot] = (unsigned long long)row | ((unsigned long long)col << 31) |
-                             ((unsigned long long)flags << 62);
+            const unsigned long long packed =
+                (unsigned long long)row | ((unsigned long long)col << 31) | ((unsigned long long)flags << 62);
+            const unsigned p = atomicAdd(lds_ncand, 1u);
+            if (p < (unsigned)CAND_LDS) {
+              lds_cand[p] = packed;
+            } else {  // block buffer full: straight to the global list
+              const unsigned long long slot = atomicAdd(a.cand_count, 1ull);
+              if ((long long)slot < a.cand_cap) a.cand[slot] = packed;
+            }
           }
         }
     // rows: reduce over the 16 lanes that share (lane >> 4); bytes stay <= 64
@@ -257,6 +278,15 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
       }
     }
     __syncthreads();
+    // flush the block's undecided pairs with ONE global atomic
+    __shared__ unsigned long long cand_base;
+    const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
+    if (tid == 0 && nlds) cand_base = atomicAdd(a.cand_count, (unsigned long long)nlds);
+    __syncthreads();
+    for (unsigned t = tid; t < nlds; t += 256) {
+      const unsigned long long slot = cand_base + t;
+      if ((long long)slot < a.cand_cap) a.cand[slot] = lds_cand[t];
+    }
     if (tid < BM) {
       const int c = lds_rc[tid];
       if (c && a.row_cnt && m0 + tid < a.nq) atomicAdd(&a.row_cnt[m0 + tid], c);
@@ -270,7 +300,8 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
 template <int MODE, int EPI>
 static int launch_sim(const SimArgs& a, hipStream_t stream) {
   constexpr int NPLANE = (MODE == CMVE_SIM_BF16X3) ? 4 : 2;
-  const size_t lds = 2 * (size_t)NPLANE * PLANE_BYTES + (EPI == EPI_RANK ? 2 * 128 * sizeof(int) : 0);
+  const size_t lds = 2 * (size_t)NPLANE * PLANE_BYTES +
+                     (EPI == EPI_RANK ? 2 * 128 * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 : 0);
   static bool attr_done = false;
   if (!attr_done) {
     CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -289,17 +320,19 @@ static int validate_pair(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mod
   CMVE_REQUIRE(q->n_pad % BM == 0 && g->n_pad % BN == 0 && q->d_pad % BK == 0, "%s: sets not packed/padded", fn);
   CMVE_REQUIRE(q->n <= q->n_pad && g->n <= g->n_pad, "%s: n > n_pad", fn);
   CMVE_REQUIRE(q->n < (1ll << 31) && g->n < (1ll << 31), "%s: set too large for int32 indices", fn);
-  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3, "%s: unknown mode %d", fn, mode);
+  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16, "%s: unknown mode %d", fn,
+               mode);
   CMVE_REQUIRE(q->hi && g->hi, "%s: hi plane missing", fn);
   if (mode == CMVE_SIM_BF16X3) CMVE_REQUIRE(q->lo && g->lo, "%s: BF16X3 needs lo planes", fn);
+  if (mode == CMVE_SIM_F16) CMVE_REQUIRE(q->h16 && g->h16, "%s: F16 needs h16 planes", fn);
   return CMVE_OK;
 }
 
-static SimArgs make_args(const cmve_rows_t* q, const cmve_rows_t* g) {
+static SimArgs make_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode) {
   SimArgs a{};
-  a.qhi = q->hi;
+  a.qhi = mode == CMVE_SIM_F16 ? q->h16 : q->hi;
   a.qlo = q->lo;
-  a.ghi = g->hi;
+  a.ghi = mode == CMVE_SIM_F16 ? g->h16 : g->hi;
   a.glo = g->lo;
   a.ldk = q->d_pad;
   a.nq = (int)q->n;
@@ -322,14 +355,15 @@ extern "C" int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_
   CMVE_REQUIRE(out && ldo >= g->n, "cmve_sim_store: bad output");
   CMVE_REQUIRE(out_dtype == CMVE_F32 || out_dtype == CMVE_F64, "cmve_sim_store: out_dtype must be F32/F64");
   if (q->n == 0 || g->n == 0) return CMVE_OK;
-  SimArgs a = make_args(q, g);
+  SimArgs a = make_args(q, g, mode);
   a.out = out;
   a.ldo = ldo;
   a.alpha = alpha;
   a.beta = beta;
   a.out_f64 = out_dtype == CMVE_F64;
-  return mode == CMVE_SIM_BF16 ? launch_sim<CMVE_SIM_BF16, EPI_STORE>(a, h->stream)
-                               : launch_sim<CMVE_SIM_BF16X3, EPI_STORE>(a, h->stream);
+  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_STORE>(a, h->stream);
+  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_STORE>(a, h->stream);
+  return launch_sim<CMVE_SIM_BF16X3, EPI_STORE>(a, h->stream);
 }
 
 // defined in rank.hip
@@ -348,7 +382,7 @@ static int rank_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, i
   if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_hi && row_lo && row_cnt, "%s: row arrays missing", fn);
   if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_hi && col_lo && col_cnt, "%s: col arrays missing", fn);
   CMVE_REQUIRE(cand && cand_count && cand_cap >= 0, "%s: candidate buffer missing", fn);
-  a = make_args(q, g);
+  a = make_args(q, g, mode);
   if (dirs & CMVE_DIR_ROW) {
     a.row_hi = row_hi;
     a.row_lo = row_lo;
@@ -378,8 +412,9 @@ extern "C" int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_
   if (dirs & CMVE_DIR_ROW) CMVE_HIP(hipMemsetAsync(row_cnt, 0, sizeof(int32_t) * q->n_pad, h->stream));
   if (dirs & CMVE_DIR_COL) CMVE_HIP(hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * g->n_pad, h->stream));
   if (q->n == 0 || g->n == 0) return CMVE_OK;
-  return mode == CMVE_SIM_BF16 ? launch_sim<CMVE_SIM_BF16, EPI_RANK>(a, h->stream)
-                               : launch_sim<CMVE_SIM_BF16X3, EPI_RANK>(a, h->stream);
+  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_RANK>(a, h->stream);
+  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_RANK>(a, h->stream);
+  return launch_sim<CMVE_SIM_BF16X3, EPI_RANK>(a, h->stream);
 }
 
 extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,

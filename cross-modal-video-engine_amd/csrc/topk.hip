@@ -69,7 +69,7 @@ __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restr
   // prefix is now the key of the k-th largest score
   const uint32_t kk = prefix;
   const float tk = __uint_as_float((kk & 0x80000000u) ? (kk & 0x7fffffffu) : ~kk);
-  const double E = score_error_bound((double)qerr[row], (double)gerr_max[mode == CMVE_SIM_BF16 ? 0 : 1], d_pad, mode);
+  const double E = score_error_bound((double)qerr[row], (double)gerr_max[mode_slot(mode)], d_pad, mode);
   const float tau = (kk == 0u) ? -INFINITY : f32_round_down((double)tk - 2.0 * E);
 
   // ---- collect the band ----
@@ -147,7 +147,8 @@ extern "C" int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_
   if (q->n == 0) return CMVE_OK;
   int st = cmve_sim_store(h, q, g, mode, 1.0f, 0.0f, scores_ws, CMVE_F32, g->n_pad);
   if (st) return st;
-  const float* qerr = mode == CMVE_SIM_BF16 ? q->err_hi : q->err_hilo;
+  const float* qerr = mode_err(q, mode);
+  CMVE_REQUIRE(qerr, "cmve_topk: set has no error plane for this mode");
 #define TK(TQ, TG)                                                                                                \
   hipLaunchKernelGGL((topk_kernel<TQ, TG>), dim3((unsigned)q->n), dim3(TOPK_THREADS), 0, h->stream, scores_ws,    \
                      g->n_pad, g->n, k, (const TQ*)q->raw, q->raw_ld, q->inv_norm, qerr, (const TG*)g->raw,       \

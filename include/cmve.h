@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 1
+#define CMVE_ABI_VERSION 2
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -39,6 +39,7 @@ enum cmve_dtype { CMVE_F32 = 0, CMVE_F64 = 1, CMVE_BF16 = 2, CMVE_I32 = 3, CMVE_
 enum cmve_sim_mode {
   CMVE_SIM_BF16 = 0,    /* hi . hi                         (one bf16 MFMA per k-step)   */
   CMVE_SIM_BF16X3 = 1,  /* hi.hi + hi.lo + lo.hi  (split-bf16, ~1e-6 of fp64 cosine)     */
+  CMVE_SIM_F16 = 2,     /* h16 . h16  fp16 plane, same MFMA rate as bf16, 8x finer rounding */
 };
 
 /* rank directions for cmve_rank_count */
@@ -59,7 +60,9 @@ enum cmve_rank_dir { CMVE_DIR_ROW = 1, CMVE_DIR_COL = 2 };
  *   inv_norm: [n_pad] fp64 1/||raw_i|| (NaN for a zero row when eps == 0)
  *   err_hi  : [n_pad] upper bound of ||x_hat_i - hi_i||_2
  *   err_hilo: [n_pad] upper bound of ||x_hat_i - hi_i - lo_i||_2
- *   err_max : [2] max over rows of err_hi / err_hilo
+ *   h16     : [n_pad, d_pad] fp16 plane of x_hat (NULL if the set has no fp16 plane)
+ *   err_h16 : [n_pad] upper bound of ||x_hat_i - h16_i||_2
+ *   err_max : [3] max over rows of err_hi / err_hilo / err_h16
  */
 typedef struct cmve_rows {
   int64_t n, d, n_pad, d_pad;
@@ -74,6 +77,8 @@ typedef struct cmve_rows {
   float* err_hilo;
   float* err_max;
   double eps;            /* normalisation epsilon: 0 = LINAS l2norm, 1e-12 = F.normalize */
+  uint16_t* h16;
+  float* err_h16;
 } cmve_rows_t;
 
 typedef struct cmve_handle* cmve_handle_t;
@@ -85,6 +90,11 @@ int cmve_create(int device, void* hip_stream, cmve_handle_t* out);
 int cmve_set_stream(cmve_handle_t h, void* hip_stream);
 int cmve_destroy(cmve_handle_t h);
 
+/* Test hook: runs crafted v_mfma_f32_16x16x32_{bf16,f16} cases on one wave and writes
+ * the 10 fp32 results (5 bf16 cases, 5 f16 cases) to out10 (device).  The rank error
+ * bound's accumulation model is asserted against these (tests/test_gpu_numerics.py). */
+int cmve_mfma_probe(cmve_handle_t h, float* out10);
+
 /* padded sizes for a [n, d] set */
 int cmve_pack_size(int64_t n, int64_t d, int64_t* n_pad, int64_t* d_pad);
 
@@ -93,8 +103,9 @@ int cmve_pack_size(int64_t n, int64_t d, int64_t* n_pad, int64_t* d_pad);
  * Replaces: LINAS-engine/evaluation.py:10-14 (l2norm), LINAS-engine/model.py:35-40
  * (l2norm, no eps), MultiFusion/src/combiner.py:134,180 and
  * MultiFusion/src/validate.py:55 (F.normalize, eps 1e-12).
- * Fills rows->{hi, lo, inv_norm, err_hi, err_hilo, err_max}; rows->raw/raw_dtype/
- * raw_ld/n/d/eps describe the input.  lo may be NULL (bf16-only set).
+ * Fills rows->{hi, lo, h16, inv_norm, err_hi, err_hilo, err_h16, err_max}; rows->raw/
+ * raw_dtype/raw_ld/n/d/eps describe the input.  lo and h16 may be NULL (planes not
+ * wanted); hi is always written.
  */
 int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* rows);
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 1
+    assert _lib.lib.cmve_abi_version() == 2
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)
@@ -42,8 +42,8 @@ def test_host_only_entry_points():
 
 def test_rows_struct_layout_matches_header():
     from cmve import _lib
-    # 4 int64 + 2 ptr + ptr + 2 int32 + int64 + 4 ptr + double = 13 * 8 bytes
-    assert C.sizeof(_lib.Rows) == 8 * 4 + 8 * 2 + 8 + 4 * 2 + 8 + 8 * 4 + 8
+    # 4 int64 + 2 ptr + ptr + 2 int32 + int64 + 4 ptr + double + 2 ptr
+    assert C.sizeof(_lib.Rows) == 8 * 4 + 8 * 2 + 8 + 4 * 2 + 8 + 8 * 4 + 8 + 8 * 2
 
 
 def test_gfx950_code_object_present():

@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench's dominant kernel (run on the GPU box via gpurun).
+#   pass 1: kernel trace + stats;  pass 2: FETCH_SIZE;  pass 3: WRITE_SIZE  (separate PMC passes)
+# then tools/traffic.py turns them into profiles/<tag>_traffic.json (read by bench.py).
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=${1:-r01}
+ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3 --no-extras"}
+OUT=$R/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/bench_trace.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras > "$OUT/bench_fetch.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras > "$OUT/bench_write.log" 2>&1
+python3 "$R/tools/traffic.py" "$OUT" "$TAG" > "$OUT/traffic.log" 2>&1
+echo "profile done: $OUT"

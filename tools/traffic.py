@@ -1,0 +1,54 @@
+"""Reduce rocprofv3 CSVs (tools/profile.sh) to per-launch figures of the bench's dominant kernel.
+
+HBM bytes = 2 * FETCH_SIZE(KiB) * 1024 + WRITE_SIZE(KiB) * 1024 per dispatch: on gfx950
+FETCH_SIZE reports half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM),
+WRITE_SIZE is exact for 16-B streaming stores.  Writes profiles/<tag>_traffic.json and copies
+the kernel stats summary to profiles/<tag>_kernel_stats.csv."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "sim_kernel<2, 1>"  # cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK>
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def main(outdir, tag):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(outdir, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    res = {}
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        vals = []
+        for r in rows(os.path.join(outdir, sub, "**", "*counter_collection.csv")):
+            name = r.get("Kernel_Name", "")
+            if "sim_kernel" in name and ("<2, 1>" in name or "ILi2ELi1E" in name) and r.get("Counter_Name") == counter:
+                vals.append(float(r["Counter_Value"]))
+        res[counter] = vals
+    f = res["FETCH_SIZE"]
+    w = res["WRITE_SIZE"]
+    out = {"kernel": "cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK>", "tag": tag,
+           "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
+           "write_kib_per_launch": (sum(w) / len(w)) if w else None}
+    if f and w:
+        out["hbm_bytes_per_launch"] = 2 * out["fetch_kib_per_launch"] * 1024 + out["write_kib_per_launch"] * 1024
+    out.update({"shard": 131072, "nq": 16384, "dim": 1024,
+                "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"})
+    json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
