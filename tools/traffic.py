@@ -23,8 +23,8 @@ def rows(pattern):
 
 
 def main(outdir, tag):
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    prof = os.path.join(root, "profiles")
+    # written under gpurun_out/ (merged back by gpurun), then copied into the repo's profiles/
+    prof = os.path.join(outdir, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(outdir, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
