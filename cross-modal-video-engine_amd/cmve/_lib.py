@@ -24,6 +24,8 @@ SIM_BF16, SIM_BF16X3, SIM_F16 = 0, 1, 2
 DIR_ROW, DIR_COL = 1, 2
 ROW_ALIGN, DIM_ALIGN = 128, 64
 TOPK_MAX = 2048
+PACK_RAW = 1
+POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 
 
 class Rows(C.Structure):
@@ -31,7 +33,7 @@ class Rows(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("d", C.c_int64), ("n_pad", C.c_int64), ("d_pad", C.c_int64),
         ("hi", C.c_void_p), ("lo", C.c_void_p),
-        ("raw", C.c_void_p), ("raw_dtype", C.c_int32), ("_pad0", C.c_int32), ("raw_ld", C.c_int64),
+        ("raw", C.c_void_p), ("raw_dtype", C.c_int32), ("flags", C.c_int32), ("raw_ld", C.c_int64),
         ("inv_norm", C.c_void_p), ("err_hi", C.c_void_p), ("err_hilo", C.c_void_p), ("err_max", C.c_void_p),
         ("eps", C.c_double),
         ("h16", C.c_void_p), ("err_h16", C.c_void_p),
@@ -52,6 +54,14 @@ SIGNATURES = {
     "cmve_pack_rows": (C.c_int, [_vp, _P(Rows)]),
     "cmve_l2norm_rows": (C.c_int, [_vp, _vp, _i32, _i64, _vp, _i32, _i64, _i64, _i64, _f64]),
     "cmve_sim_store": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _f32, _f32, _vp, _i32, _i64]),
+    "cmve_linear": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64]),
+    "cmve_collate_frames": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
+    "cmve_temporal_pool": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "cmve_triplet_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "cmve_triplet_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64]),
+    "cmve_infonce_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "cmve_infonce_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp, _vp, _vp, _i64]),
+    "cmve_gemm_f32": (C.c_int, [_vp, _i32, _i32, _i64, _i64, _i64, _f32, _vp, _i64, _vp, _i64, _f32, _vp, _i64]),
     "cmve_gt_thresholds": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp]),
     "cmve_rank_count": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _i64, _vp]),
@@ -69,7 +79,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -86,7 +86,7 @@ class RowSet:
     """
 
     def __init__(self, x, eps: float = 0.0, with_lo: bool = True, device: Optional[torch.device] = None,
-                 with_f16: bool = True):
+                 with_f16: bool = True, raw_rows: bool = False):
         device = device or default_device()
         raw = to_device(x, device)
         if raw.dim() != 2:
@@ -109,7 +109,7 @@ class RowSet:
         self.err_max = torch.empty(3, dtype=torch.float32, device=device)
         self.desc = Rows(n=n, d=d, n_pad=n_pad, d_pad=d_pad, hi=self.hi.data_ptr(),
                          lo=self.lo.data_ptr() if self.lo is not None else None,
-                         raw=raw.data_ptr() if n else None, raw_dtype=_dtype_code(raw), _pad0=0,
+                         raw=raw.data_ptr() if n else None, raw_dtype=_dtype_code(raw), flags=_lib.PACK_RAW if raw_rows else 0,
                          raw_ld=raw.stride(0) if n else d, inv_norm=self.inv_norm.data_ptr(),
                          err_hi=self.err_hi.data_ptr(), err_hilo=self.err_hilo.data_ptr(),
                          err_max=self.err_max.data_ptr(), eps=self.eps,

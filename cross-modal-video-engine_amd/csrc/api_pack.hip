@@ -36,7 +36,7 @@ int check_launch(const char* what) {
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ raw, int64_t ld, int64_t n,
-                                                        int64_t d, int64_t n_pad, int64_t d_pad, double eps,
+                                                        int64_t d, int64_t n_pad, int64_t d_pad, double eps, int flags,
                                                         uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                                         uint16_t* __restrict__ h16, double* __restrict__ inv_norm,
                                                         float* __restrict__ err_hi, float* __restrict__ err_hilo,
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
   ss = wave_sum(ss);
   const double nrm = sqrt(ss);
   // eps == 0: LINAS l2norm (X / norm, NaN on a zero row); eps > 0: F.normalize
-  const double inv = eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm;
+  const double inv = (flags & CMVE_PACK_RAW) ? 1.0 : (eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm);
   double e1 = 0.0, e2 = 0.0, e3 = 0.0;
   for (int64_t k = lane; k < d_pad; k += 64) {
     if (k < d) {
@@ -194,11 +194,11 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
   dim3 grid((unsigned)((r->n_pad + 3) / 4)), block(256);
   if (r->raw_dtype == CMVE_F32)
     hipLaunchKernelGGL(pack_rows_kernel<float>, grid, block, 0, h->stream, (const float*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
+                       r->d, r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
                        r->err_h16, r->err_max);
   else if (r->raw_dtype == CMVE_F64)
     hipLaunchKernelGGL(pack_rows_kernel<double>, grid, block, 0, h->stream, (const double*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
+                       r->d, r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
                        r->err_h16, r->err_max);
   else {
     set_error("cmve_pack_rows: raw_dtype must be CMVE_F32 or CMVE_F64");

@@ -24,7 +24,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int PLANE_BYTES = BM * BK * 2;  // 16 KiB
-constexpr int EPI_STORE = 0, EPI_RANK = 1;
+constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2;
 constexpr int CAND_LDS = 1024;  // per-block undecided-pair buffer (one global atomic per block)
 
 struct SimArgs {
@@ -36,6 +36,13 @@ struct SimArgs {
   int nq, ng;
   int nblk_m, nblk_n;
   int nk;
+  // linear epilogue: v = acc + bias; relu; + resid; v * bn_scale + bn_shift
+  const float* bias;
+  const float* bn_scale;
+  const float* bn_shift;
+  const float* resid;
+  int64_t ldr;
+  int relu;
   // store
   void* out;
   int64_t ldo;
@@ -182,7 +189,34 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
   const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
   const int cbase = n0 + wc * 64 + (lane & 15);
 
-  if constexpr (EPI == EPI_STORE) {
+  if constexpr (EPI == EPI_LINEAR) {
+    float bj[4], sj[4], hj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + j * 16;
+      const bool ok = col < a.ng;
+      bj[j] = (a.bias && ok) ? a.bias[col] : 0.f;
+      sj[j] = (a.bn_scale && ok) ? a.bn_scale[col] : 1.f;
+      hj[j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + i * 16 + r;
+        if (row >= a.nq) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = cbase + j * 16;
+          if (col >= a.ng) continue;
+          float v = acc[i][j][r] + bj[j];
+          if (a.relu) v = fmaxf(v, 0.f);
+          if (a.resid) v = a.resid[(int64_t)row * a.ldr + col] + v;
+          if (a.bn_scale) v = v * sj[j] + hj[j];
+          ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
+        }
+      }
+  } else if constexpr (EPI == EPI_STORE) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -440,4 +474,28 @@ extern "C" int cmve_rank_count(cmve_handle_t h, const cmve_rows_t* q, const cmve
                           cand_count);
   if (st) return st;
   return cmve_rank_fixup(h, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, cand_count);
+}
+
+extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_rows_t* w, int32_t mode, const float* bias,
+                           const float* bn_scale, const float* bn_shift, const float* resid, int64_t ldr, int32_t relu,
+                           float* out, int64_t ldo) {
+  CMVE_REQUIRE(h, "cmve_linear: NULL handle");
+  int st = validate_pair(x, w, mode, "cmve_linear");
+  if (st) return st;
+  CMVE_REQUIRE(out && ldo >= w->n, "cmve_linear: bad output");
+  CMVE_REQUIRE((bn_scale == nullptr) == (bn_shift == nullptr), "cmve_linear: bn_scale and bn_shift go together");
+  CMVE_REQUIRE(!resid || ldr >= w->n, "cmve_linear: bad residual leading dimension");
+  if (x->n == 0 || w->n == 0) return CMVE_OK;
+  SimArgs a = make_args(x, w, mode);
+  a.out = out;
+  a.ldo = ldo;
+  a.bias = bias;
+  a.bn_scale = bn_scale;
+  a.bn_shift = bn_shift;
+  a.resid = resid;
+  a.ldr = ldr;
+  a.relu = relu;
+  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_LINEAR>(a, h->stream);
+  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_LINEAR>(a, h->stream);
+  return launch_sim<CMVE_SIM_BF16X3, EPI_LINEAR>(a, h->stream);
 }

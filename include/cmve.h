@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 2
+#define CMVE_ABI_VERSION 3
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -44,6 +44,9 @@ enum cmve_sim_mode {
 
 /* rank directions for cmve_rank_count */
 enum cmve_rank_dir { CMVE_DIR_ROW = 1, CMVE_DIR_COL = 2 };
+
+/* cmve_rows_t.flags */
+#define CMVE_PACK_RAW 1   /* pack the rows as given (no L2 normalisation): GEMM operands of cmve_linear */
 
 /* Tile geometry of the packed planes: rows padded to CMVE_ROW_ALIGN,
  * dimension padded to CMVE_DIM_ALIGN (zero fill). */
@@ -70,7 +73,7 @@ typedef struct cmve_rows {
   uint16_t* lo;
   const void* raw;
   int32_t raw_dtype;
-  int32_t _pad0;
+  int32_t flags;         /* CMVE_PACK_* */
   int64_t raw_ld;
   double* inv_norm;
   float* err_hi;
@@ -128,6 +131,67 @@ int cmve_l2norm_rows(cmve_handle_t h, const void* x, int32_t x_dtype, int64_t ld
  */
 int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode,
                    float alpha, float beta, void* out, int32_t out_dtype, int64_t ldo);
+
+/*
+ * K3 -- projection GEMM with fused epilogue (MFC / Latent_mapping in eval mode,
+ * LINAS-engine/model.py:97-116,374-381):  out[i, j] = BN( resid[i, j] + act( x_i . w_j + bias[j] ) )
+ * with act = ReLU if relu != 0, resid optional (the fc2..fc4 residual layers, model.py:104-109),
+ * BN eval as a per-column affine v * bn_scale + bn_shift (both NULL = no BN).  x [N, K] and
+ * w [F_out, K] (torch nn.Linear layout) are packed with CMVE_PACK_RAW; mode CMVE_SIM_BF16X3
+ * gives ~1e-6 relative error (the fp32 reference's own rounding is ~1e-7).  out fp32 [N, F_out].
+ */
+int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_rows_t* w, int32_t mode,
+                const float* bias, const float* bn_scale, const float* bn_shift,
+                const float* resid, int64_t ldr, int32_t relu, float* out, int64_t ldo);
+
+/*
+ * K2 -- temporal pooling.  collate: ragged frames [sum T_b, F] (row offsets[B+1]) ->
+ * videos [B, t_max, F] (first min(max_len, T_b) frames, zero padded), origin [B, F] = mean
+ * over ALL frames, mask [B, t_max] (LINAS-engine/util/tag_data_provider.py:91-109).
+ */
+int cmve_collate_frames(cmve_handle_t h, const float* frames, int64_t ldf, const int64_t* offsets,
+                        int64_t B, int64_t F, int32_t max_len, int32_t t_max,
+                        float* videos, float* origin, float* mask);
+
+/* pool x[b, t, f] (strides in elements, f contiguous) over t -> out [B, F]:
+ * mode 0 MEAN_VALID (t < lengths[b], LINAS-engine/model.py:152-156), 1 MEAN_ALL
+ * (MultiFusion/src/combiner.py:140-143, MCT recognizer2d.py:76-83), 2 MAX_MASKED_ZERO
+ * (max_t x*mask, masked steps contribute 0: model.py:157-158), 3 MAX_ALL (model.py:166). */
+int cmve_temporal_pool(cmve_handle_t h, const float* x, int64_t stride_b, int64_t stride_t,
+                       int64_t B, int64_t T, int64_t F, const int32_t* lengths, int32_t mode,
+                       float* out, int64_t ldo);
+
+/*
+ * K6 -- TripletLoss (LINAS-engine/loss.py:83-153) over a square score matrix S [B, B]
+ * (S = im . s^T, rows = videos, columns = captions, cosine_sim loss.py:7-10).
+ * dir bit 1 = cost_s (v2t, max over dim 1), bit 2 = cost_im (t2v, max over dim 0);
+ * max_violation: hardest negative (first index on ties, as torch.max), else sum of all costs;
+ * mean_style: cost_style 'mean'.  loss = device f32[1]; row_/col_ val/arg [B] are workspace
+ * the backward reuses.  bwd writes dL/dS [B, B] for upstream gradient *g (device f32).
+ */
+int cmve_triplet_fwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float margin,
+                     int32_t max_violation, int32_t dir, int32_t mean_style, float* loss,
+                     float* row_val, int32_t* row_arg, float* col_val, int32_t* col_arg);
+int cmve_triplet_bwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float margin,
+                     int32_t max_violation, int32_t dir, int32_t mean_style, const float* g,
+                     const int32_t* row_arg, const int32_t* col_arg, float* dS, int64_t ldd);
+
+/*
+ * K7 -- InfoNCE on logits scale * S: row half = CE(logits, arange) (MultiFusion/src/combiner_train.py:
+ * 318,367-372), col half = CE(logits^T, arange) (MCT/mmaction/models/backbones/clip.py:383-386).
+ * dir 1 row, 2 col, 3 both = (row + col) / 2.  loss3 (device f32[3]) = {row, col, selected};
+ * row_lse/col_lse (f64 [B]) and row_loss/col_loss (f32 [B]) are workspace kept for the backward.
+ */
+int cmve_infonce_fwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float scale, int32_t dir,
+                     float* loss3, double* row_lse, double* col_lse, float* row_loss, float* col_loss);
+int cmve_infonce_bwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float scale, int32_t dir,
+                     const float* g, const double* row_lse, const double* col_lse, float* dS, int64_t ldd);
+
+/* fp32 GEMM for the loss gradient products: C = alpha * op(A) . op(B) + beta * C
+ * (op = transpose when trans* != 0; row-major; fp32 FMA chain). */
+int cmve_gemm_f32(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K,
+                  float alpha, const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
+                  float* C, int64_t ldc);
 
 /*
  * K5a -- exact fp64 GT scores and rank thresholds for one direction.
