@@ -78,7 +78,7 @@ def test_latent_mapping_eval(golden, name):
     lm.load_state_dict({k: torch.from_numpy(v) for k, v in _sd(g).items()})
     lm.eval()
     y = lm(torch.from_numpy(g["x"]).cuda())
-    np.testing.assert_allclose(y.cpu().numpy(), g["y"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(y.cpu().numpy(), g["y"], rtol=0, atol=1e-5)  # fp32 ref ~1e-6 + split-bf16 per layer
 
 
 @pytest.mark.parametrize("name", ["mv_sum_all", "mv_sum_all_b8", "mv_mean_all", "sum_all", "mv_sum_t2v", "mv_sum_v2t",
