@@ -57,6 +57,9 @@ SIGNATURES = {
     "cmve_linear": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64]),
     "cmve_collate_frames": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
     "cmve_temporal_pool": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "cmve_layernorm": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _i64]),
+    "cmve_mha_1q": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64]),
+    "cmve_fuse_combine": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f64, _vp]),
     "cmve_triplet_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     "cmve_triplet_bwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64]),
     "cmve_infonce_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp, _vp, _vp, _vp]),

@@ -1,0 +1,171 @@
+"""Mirror of MultiFusion's ``Combiner`` (MultiFusion/src/combiner.py:81-180) on libcmve.so (eval).
+
+Same constructor, submodule names and state-dict keys as the reference, so a reference
+checkpoint ``{'Combiner': state_dict}`` (MultiFusion/src/inference.py:213-223) loads directly.
+``combine_features`` / ``forward`` / ``time_process`` run on the HIP kernels:
+  conv1x1 on the raw (b*f, d, 4, 4) reshape, projections, in/out projections, MLP, combiner
+  and dynamic-scalar layers -> cmve_linear (split-bf16 MFMA, fused bias/act/residual epilogue);
+  LayerNorm -> cmve_layernorm; the 1-query x 128-key attention over the batch-mixing
+  p_s_m.reshape(l*f, b, d) (combiner.py:164-165) -> cmve_mha_1q; v.mean(0) and time_process ->
+  cmve_temporal_pool; the residual combine + F.normalize -> cmve_fuse_combine.
+PyTorch only re-lays memory (reshape / transpose / cat), exactly as the reference's reshapes.
+The batch-composition dependence of the reference is therefore reproduced.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from .. import engine
+from .._lib import lib, check, SIM_BF16X3
+from ..linas.model import linear_fused, temporal_pool, _PackedWeight
+
+ACT_NONE, ACT_RELU, ACT_QUICKGELU, ACT_SIGMOID = 0, 1, 2, 3
+
+
+def _linear(x, w, b, act=ACT_NONE, resid=None, packed=None):
+    x = x.detach().float().contiguous()
+    xr = engine.RowSet(x, with_lo=True, with_f16=False, raw_rows=True, device=x.device)
+    wr = packed.get(w) if packed is not None else _PackedWeight().get(w)
+    out = torch.empty((x.shape[0], w.shape[0]), dtype=torch.float32, device=x.device)
+    bb = b.detach().float().contiguous() if b is not None else None
+    r = resid.contiguous() if resid is not None else None
+    check(lib.cmve_linear(engine.handle(x.device), engine.C.byref(xr.desc), engine.C.byref(wr.desc), SIM_BF16X3,
+                          engine._ptr(bb), None, None, engine._ptr(r), r.stride(0) if r is not None else 0, act,
+                          engine._ptr(out), out.stride(0)), "cmve_linear")
+    return out
+
+
+def _layernorm(x, ln: nn.LayerNorm):
+    x = x.contiguous().float()
+    y = torch.empty_like(x)
+    n, d = x.shape
+    check(lib.cmve_layernorm(engine.handle(x.device), engine._ptr(x), x.stride(0), n, d,
+                             engine._ptr(ln.weight.detach().float().contiguous()),
+                             engine._ptr(ln.bias.detach().float().contiguous()), float(ln.eps), engine._ptr(y),
+                             y.stride(0)), "cmve_layernorm")
+    return y
+
+
+class QuickGELU(nn.Module):
+    def forward(self, x):
+        return x * torch.sigmoid(1.702 * x)
+
+
+class ResidualAttentionBlock(nn.Module):
+    """combiner.py:19-43 -- parameters only; the forward is fused in Combiner.combine_features."""
+
+    def __init__(self, d_model: int, n_head: int):
+        super().__init__()
+        self.attn = nn.MultiheadAttention(d_model, n_head)
+        self.ln_1 = nn.LayerNorm(d_model)
+        self.mlp = nn.Sequential(OrderedDict([("c_fc", nn.Linear(d_model, d_model * 4)), ("gelu", QuickGELU()),
+                                              ("c_proj", nn.Linear(d_model * 4, d_model))]))
+        self.ln_2 = nn.LayerNorm(d_model)
+
+
+class Combiner(nn.Module):
+    def __init__(self, clip_feature_dim: int, projection_dim: int, hidden_dim: int):
+        super().__init__()
+        self.text_projection_layer = nn.Linear(clip_feature_dim, projection_dim)
+        self.image_projection_layer = nn.Linear(clip_feature_dim, projection_dim)
+        self.dropout1 = nn.Dropout(0.5)
+        self.dropout2 = nn.Dropout(0.5)
+        self.combiner_layer = nn.Linear(projection_dim * 2, hidden_dim)
+        self.output_layer = nn.Linear(hidden_dim, clip_feature_dim)
+        self.dropout3 = nn.Dropout(0.5)
+        self.dynamic_scalar = nn.Sequential(nn.Linear(projection_dim * 2, hidden_dim), nn.ReLU(), nn.Dropout(0.5),
+                                            nn.Linear(hidden_dim, 1), nn.Sigmoid())
+        self.logit_scale = 100
+        self.m_remained = nn.Conv2d(clip_feature_dim, clip_feature_dim, (1, 1))
+        self.m_residual = nn.Linear(clip_feature_dim, clip_feature_dim)
+        self.nhead = 8
+        self.self_attn_1 = ResidualAttentionBlock(clip_feature_dim, self.nhead)
+        self.dropout4 = nn.Dropout(0.5)
+        self.dropout6 = nn.Dropout(0.5)
+        self.dropout7 = nn.Dropout(0.5)
+        self._pk = {}
+        self._cat_key = None
+        self._cat_w = self._cat_b = None
+
+    def _p(self, name):
+        return self._pk.setdefault(name, _PackedWeight())
+
+    def _hidden_cat(self):
+        """combiner_layer and dynamic_scalar[0] read the same input: one GEMM with both weights."""
+        a, b = self.combiner_layer, self.dynamic_scalar[0]
+        key = (a.weight.data_ptr(), a.weight._version, b.weight.data_ptr(), b.weight._version)
+        if self._cat_key != key:
+            self._cat_w = torch.cat([a.weight.detach(), b.weight.detach()], 0).float().contiguous()
+            self._cat_b = torch.cat([a.bias.detach(), b.bias.detach()], 0).float().contiguous()
+            self._cat_key = key
+        return self._cat_w, self._cat_b
+
+    def time_process(self, fea):
+        """combiner.py:140-143: mean over the frame axis."""
+        return temporal_pool(fea, "mean")
+
+    @torch.no_grad()
+    def combine_features(self, image_features, text_features):
+        if self.training:
+            raise NotImplementedError("cmve Combiner: eval-mode forward only (training is SURVEY 8f 'next')")
+        ref_high, ref_mid = image_features
+        ref_high = ref_high.float()
+        ref_mid = ref_mid.float()
+        text = text_features.float().contiguous()
+        b, f, l, d = ref_mid.size()
+        n = b * f
+        # conv1x1 over the raw reshape (b*f, -1, 4, 4) (combiner.py:159): channel c = elements c*16 .. c*16+15
+        C = ref_mid[0, 0].numel() // 16
+        xt = ref_mid.reshape(n, C, 16).transpose(1, 2).reshape(n * 16, C)
+        wc = self.m_remained.weight.view(self.m_remained.weight.shape[0], -1)
+        y = _linear(xt, wc, self.m_remained.bias, ACT_RELU, packed=self._p("m_remained"))
+        p_s_m = y.view(n, 16, -1).transpose(1, 2).reshape(b, f, l, -1)              # relu(conv).reshape(b,f,l,-1)
+        p_r_m = _linear(text, self.m_residual.weight, self.m_residual.bias, ACT_RELU, packed=self._p("m_residual"))
+        # ResidualAttentionBlock(q = p_r_m [1,b,d], k = v = p_s_m.reshape(l*f, b, d))  combiner.py:38-43,164-165
+        blk = self.self_attn_1
+        kv_in = p_s_m.reshape(l * f * b, d)                 # row t*b + bb  ==  [t, bb] of reshape(l*f, b, d)
+        kv_ln = _layernorm(kv_in, blk.ln_1)
+        q_ln = _layernorm(p_r_m, blk.ln_1)
+        W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
+        q = _linear(q_ln, W[:d], Bi[:d], packed=self._p("in_q"))
+        kv = _linear(kv_ln, W[d:], Bi[d:], packed=self._p("in_kv"))          # [l*f*b, 2d]: K | V
+        attn = torch.empty((b, d), dtype=torch.float32, device=text.device)
+        check(lib.cmve_mha_1q(engine.handle(text.device), engine._ptr(q), q.stride(0), engine._ptr(kv), kv.stride(0), d,
+                              b, l * f, self.nhead, d // self.nhead, engine._ptr(attn), attn.stride(0)), "cmve_mha_1q")
+        v3 = p_s_m.reshape(l * f, b, d)
+        v_mean = temporal_pool(v3.transpose(0, 1), "mean")                    # v.mean(dim=0), strided view
+        x = _linear(attn, blk.attn.out_proj.weight, blk.attn.out_proj.bias, resid=v_mean, packed=self._p("out_proj"))
+        h = _linear(_layernorm(x, blk.ln_2), blk.mlp.c_fc.weight, blk.mlp.c_fc.bias, ACT_QUICKGELU,
+                    packed=self._p("c_fc"))
+        based = _linear(h, blk.mlp.c_proj.weight, blk.mlp.c_proj.bias, resid=x, packed=self._p("c_proj"))
+        # projections, combiner and dynamic scalar (combiner.py:168-175)
+        ref_mean = self.time_process(ref_high)
+        tp = _linear(text, self.text_projection_layer.weight, self.text_projection_layer.bias, ACT_RELU,
+                     packed=self._p("tp"))
+        ip = _linear(ref_mean, self.image_projection_layer.weight, self.image_projection_layer.bias, ACT_RELU,
+                     packed=self._p("ip"))
+        raw = torch.cat((ip, tp), -1)
+        wcat, bcat = self._hidden_cat()
+        hid = _linear(raw, wcat, bcat, ACT_RELU, packed=self._p("hidden_cat"))
+        hd = self.combiner_layer.weight.shape[0]
+        combined = hid[:, :hd]
+        ds = _linear(hid[:, hd:], self.dynamic_scalar[3].weight, self.dynamic_scalar[3].bias, ACT_SIGMOID,
+                     packed=self._p("ds3"))
+        yo = _linear(combined, self.output_layer.weight, self.output_layer.bias, packed=self._p("out"))
+        out = torch.empty_like(yo)
+        check(lib.cmve_fuse_combine(engine.handle(text.device), engine._ptr(yo), engine._ptr(ds.contiguous()),
+                                    engine._ptr(text), engine._ptr(ref_mean), engine._ptr(based.contiguous()), b, d,
+                                    1e-12, engine._ptr(out)), "cmve_fuse_combine")
+        return out
+
+    @torch.no_grad()
+    def forward(self, image_features, text_features, target_features):
+        """combiner.py:121-138: logits = 100 * pred @ normalize(time_process(target[0])).T"""
+        pred = self.combine_features(image_features, text_features)
+        tgt = self.time_process(target_features[0].float())
+        qp = engine.RowSet(pred, with_lo=True, with_f16=False, raw_rows=True, device=pred.device)
+        tg = engine.RowSet(tgt, eps=1e-12, with_lo=True, with_f16=False, device=pred.device)
+        return engine.sim_store(qp, tg, alpha=float(self.logit_scale), mode=SIM_BF16X3)

@@ -210,7 +210,9 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
           const int col = cbase + j * 16;
           if (col >= a.ng) continue;
           float v = acc[i][j][r] + bj[j];
-          if (a.relu) v = fmaxf(v, 0.f);
+          if (a.relu == 1) v = fmaxf(v, 0.f);                                   // ReLU
+          else if (a.relu == 2) v = v / (1.f + expf(-1.702f * v));            // QuickGELU x*sigmoid(1.702x)
+          else if (a.relu == 3) v = 1.f / (1.f + expf(-v));                   // Sigmoid
           if (a.resid) v = a.resid[(int64_t)row * a.ldr + col] + v;
           if (a.bn_scale) v = v * sj[j] + hj[j];
           ((float*)a.out)[(int64_t)row * a.ldo + col] = v;

@@ -135,7 +135,8 @@ int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, 
 /*
  * K3 -- projection GEMM with fused epilogue (MFC / Latent_mapping in eval mode,
  * LINAS-engine/model.py:97-116,374-381):  out[i, j] = BN( resid[i, j] + act( x_i . w_j + bias[j] ) )
- * with act = ReLU if relu != 0, resid optional (the fc2..fc4 residual layers, model.py:104-109),
+ * with act (`relu` argument) 0 none, 1 ReLU, 2 QuickGELU x*sigmoid(1.702x), 3 sigmoid
+ * (MultiFusion/src/combiner.py:7-9,105-106), resid optional (the fc2..fc4 residual layers, model.py:104-109),
  * BN eval as a per-column affine v * bn_scale + bn_shift (both NULL = no BN).  x [N, K] and
  * w [F_out, K] (torch nn.Linear layout) are packed with CMVE_PACK_RAW; mode CMVE_SIM_BF16X3
  * gives ~1e-6 relative error (the fp32 reference's own rounding is ~1e-7).  out fp32 [N, F_out].
@@ -160,6 +161,21 @@ int cmve_collate_frames(cmve_handle_t h, const float* frames, int64_t ldf, const
 int cmve_temporal_pool(cmve_handle_t h, const float* x, int64_t stride_b, int64_t stride_t,
                        int64_t B, int64_t T, int64_t F, const int32_t* lengths, int32_t mode,
                        float* out, int64_t ldo);
+
+/*
+ * K8/K9 -- non-GEMM pieces of MultiFusion Combiner.combine_features (MultiFusion/src/combiner.py:19-43,146-180):
+ *   cmve_layernorm: y = LN(x) * gamma + beta (fp32 LayerNorm subclass, combiner.py:11-17)
+ *   cmve_mha_1q: one query per batch element b (q [B, H*dh]) over T keys whose projected K/V rows
+ *     are row t*B + b of kv (K at column 0, V at column v_off): the raw p_s_m.reshape(l*f, b, d)
+ *     of combiner.py:164-165, which mixes batch rows -- reproduced, not fixed.  Scaled by dh^-0.5.
+ *   cmve_fuse_combine: out = normalize(((y + ds*text) + (1-ds)*ref) + relu(based), eps)  (combiner.py:166,178-180)
+ */
+int cmve_layernorm(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d,
+                   const float* gamma, const float* beta, double eps, float* y, int64_t ldy);
+int cmve_mha_1q(cmve_handle_t h, const float* q, int64_t ldq, const float* kv, int64_t ldkv, int64_t v_off,
+                int32_t B, int32_t T, int32_t H, int32_t dh, float* out, int64_t ldo);
+int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* ds, const float* text, const float* ref,
+                      const float* based, int64_t n, int64_t d, double eps, float* out);
 
 /*
  * K6 -- TripletLoss (LINAS-engine/loss.py:83-153) over a square score matrix S [B, B]

@@ -43,3 +43,75 @@ def gallery_queries(seed=2, n_v=20000, n_q=16, d=1024, sigma=10.0):
 def bench_shard(seed, n_v, d=1024, dtype=np.float32):
     rng = np.random.default_rng(seed)
     return rng.standard_normal((n_v, d), dtype=np.float32).astype(dtype)
+
+
+def multifusion_ranking_case(tsv_rows, n_gallery=2048, d=640, frames=8, seed=3, sigma=7.0):
+    """(ix) MultiFusion ranking fixture inputs: the first triplets of the shipped val split
+    (idx, ref, target, ...) and a sub-gallery of `n_gallery` integer video names containing every
+    ref/target, with synthetic CLIP-like high features [n_gallery, frames, d] and predictions =
+    normalize(mean_f(target features) + sigma * noise).  Query 5's target is set to its reference
+    (the 'never retrieved' quirk of MultiFusion/src/validate.py:76-83)."""
+    rng = np.random.default_rng(seed)
+    refs = [int(r[1]) for r in tsv_rows]
+    tgts = [int(r[2]) for r in tsv_rows]
+    if len(tgts) > 5:
+        tgts[5] = refs[5]
+    need = sorted(set(refs) | set(tgts))
+    pool = np.setdiff1d(np.arange(44493), need)
+    extra = rng.choice(pool, size=n_gallery - len(need), replace=False)
+    names = np.array(sorted(set(need) | set(extra.tolist())), np.int64)
+    feats = rng.standard_normal((n_gallery, frames, d), dtype=np.float32)
+    pos = {int(n): i for i, n in enumerate(names)}
+    tmean = feats[[pos[t] for t in tgts]].mean(axis=1)
+    pred = tmean / np.linalg.norm(tmean, axis=1, keepdims=True) + sigma * rng.standard_normal(tmean.shape).astype(
+        np.float32) / np.sqrt(d)
+    pred = (pred / np.linalg.norm(pred, axis=1, keepdims=True)).astype(np.float32)
+    return names, feats, pred, refs, tgts
+
+
+COMBINER_SHAPES = [
+    ("text_projection_layer.weight", (2560, 640)), ("text_projection_layer.bias", (2560,)),
+    ("image_projection_layer.weight", (2560, 640)), ("image_projection_layer.bias", (2560,)),
+    ("combiner_layer.weight", (5120, 5120)), ("combiner_layer.bias", (5120,)),
+    ("output_layer.weight", (640, 5120)), ("output_layer.bias", (640,)),
+    ("dynamic_scalar.0.weight", (5120, 5120)), ("dynamic_scalar.0.bias", (5120,)),
+    ("dynamic_scalar.3.weight", (1, 5120)), ("dynamic_scalar.3.bias", (1,)),
+    ("m_remained.weight", (640, 640, 1, 1)), ("m_remained.bias", (640,)),
+    ("m_residual.weight", (640, 640)), ("m_residual.bias", (640,)),
+    ("self_attn_1.attn.in_proj_weight", (1920, 640)), ("self_attn_1.attn.in_proj_bias", (1920,)),
+    ("self_attn_1.attn.out_proj.weight", (640, 640)), ("self_attn_1.attn.out_proj.bias", (640,)),
+    ("self_attn_1.ln_1.weight", (640,)), ("self_attn_1.ln_1.bias", (640,)),
+    ("self_attn_1.mlp.c_fc.weight", (2560, 640)), ("self_attn_1.mlp.c_fc.bias", (2560,)),
+    ("self_attn_1.mlp.c_proj.weight", (640, 2560)), ("self_attn_1.mlp.c_proj.bias", (640,)),
+    ("self_attn_1.ln_2.weight", (640,)), ("self_attn_1.ln_2.bias", (640,)),
+]
+
+
+def combiner_state(seed=11):
+    """Deterministic Combiner(640, 2560, 5120) weights (64.7M params) in state-dict order:
+    weights ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch's default Linear init range), biases
+    ~ 0.05 N(0,1), LayerNorm gain 1 + 0.1 N(0,1).  Both the golden script (loading them into the
+    reference module) and the GPU test regenerate them, so no checkpoint is stored."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for name, shape in COMBINER_SHAPES:
+        if name.endswith("ln_1.weight") or name.endswith("ln_2.weight"):
+            v = 1.0 + 0.1 * rng.standard_normal(shape, dtype=np.float32)
+        elif name.endswith("bias"):
+            v = 0.05 * rng.standard_normal(shape, dtype=np.float32)
+        else:
+            fan_in = int(np.prod(shape[1:]))
+            bound = 1.0 / np.sqrt(fan_in)
+            v = rng.uniform(-bound, bound, size=shape).astype(np.float32)
+        sd[name] = v.astype(np.float32)
+    return sd
+
+
+def combiner_inputs(b, seed, frames=8, tokens=16, d=640):
+    """ref high [b, f, d], ref middle [b, f, l, d], text [b, d], target high [b, f, d] (fp32)."""
+    rng = np.random.default_rng(seed)
+    high = rng.standard_normal((b, frames, d), dtype=np.float32)
+    mid = rng.standard_normal((b, frames, tokens, d), dtype=np.float32)
+    text = rng.standard_normal((b, d), dtype=np.float32)
+    tgt = rng.standard_normal((b, frames, d), dtype=np.float32)
+    return high, mid, text, tgt
