@@ -22,7 +22,7 @@ CMVE_OK = 0
 CMVE_F32, CMVE_F64, CMVE_BF16, CMVE_I32, CMVE_I64 = 0, 1, 2, 3, 4
 SIM_BF16, SIM_BF16X3, SIM_F16 = 0, 1, 2
 DIR_ROW, DIR_COL = 1, 2
-ROW_ALIGN, DIM_ALIGN = 128, 64
+ROW_ALIGN, DIM_ALIGN = 256, 64
 TOPK_MAX = 2048
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3

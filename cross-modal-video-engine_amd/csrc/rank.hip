@@ -100,8 +100,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
     const uint32_t flags = (uint32_t)(u >> 62);
     const double s = cos64(qraw + i * ldq, graw + j * ldg, qinv[i], ginv[j], d, lane);
     if (lane == 0) {
-      if ((flags & 1u) && s > row_sgt[i]) atomicAdd(&row_cnt[i], 1);
-      if ((flags & 2u) && s > col_sgt[j]) atomicAdd(&col_cnt[j], 1);
+      if ((flags & 1u) && row_sgt && s > row_sgt[i]) atomicAdd(&row_cnt[i], 1);
+      if ((flags & 2u) && col_sgt && s > col_sgt[j]) atomicAdd(&col_cnt[j], 1);
     }
   }
 }

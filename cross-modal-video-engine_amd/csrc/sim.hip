@@ -1,17 +1,21 @@
-// K4: N_q x N_g cosine-similarity GEMM on bf16 MFMA (gfx950), with fused epilogues.
+// K4: N_q x N_g cosine-similarity GEMM on bf16 / fp16 MFMA (gfx950), with fused epilogues.
 //
-//   EPI_STORE : out[i,j] = alpha * s_ij + beta            (cal_error / cal_simi / logits)
-//   EPI_RANK  : per-row and per-column "score > threshold" counts + undecided-pair list
-//               (the GT rank of LINAS-engine/util/metrics.py:137-147 without the matrix)
+//   EPI_STORE  : out[i,j] = alpha * s_ij + beta            (cal_error / cal_simi / logits)
+//   EPI_RANK   : per-row and per-column "score > threshold" counts + undecided-pair list
+//                (the GT rank of LINAS-engine/util/metrics.py:137-147 without the matrix)
+//   EPI_LINEAR : BN(resid + act(x.w + bias))               (MFC / Combiner projections)
 //
-// Geometry: 256 threads = 4 waves (2 x 2), block tile 128 (q rows) x 128 (g rows),
-// K step 64, each wave owns 64 x 64 = 4 x 4 tiles of v_mfma_f32_16x16x32_bf16.
-// Staging: global_load_lds_dwordx4 (16 B / lane, 1 KiB per wave-instruction) into a
-// lane-linear LDS image, 2 stages; bank conflicts removed by an XOR swizzle applied
-// to the GLOBAL source chunk (chunk ^ (row & 7)) and the matching ds_read_b128 address.
-// Grid: XCD-aware -- each XCD gets a contiguous range of the logical tile order and the
-// logical order walks 8 gallery tiles x all query tiles, so the 64 co-resident blocks of
-// an XCD share 8 G tiles and 8 Q tiles in its 4 MiB L2.
+// Geometry (template WM x WN waves, each wave TM x 4 tiles of v_mfma_f32_16x16x32):
+//   G128: 2 x 2 waves, 64 x 64 per wave  -> 128 x 128 block tile, 256 threads, 2 blocks / CU
+//   G256: 2 x 4 waves, 128 x 64 per wave -> 256 x 256 block tile, 512 threads, 1 block / CU
+// The 256^2 tile doubles the FLOP per staged byte (128 vs 64 FLOP/B), which a 128^2 tile
+// cannot feed from L2 at the MFMA rate (~63 B/clk/CU needed vs ~56 available); G256 is the
+// default for bf16/fp16 problems with >= 512 tiles, G128 for split-bf16 (4 planes) and small
+// problems.  K step 64; staging by global_load_lds_dwordx4 (16 B / lane, 1 KiB per wave
+// instruction) into a lane-linear LDS image, 2 stages; bank conflicts removed by an XOR
+// swizzle applied to the GLOBAL source chunk (chunk ^ (row & 7)) and the matching
+// ds_read_b128 address.  Grid: XCD-aware -- each XCD gets a contiguous range of the logical
+// tile order, which walks 8 gallery tiles x all query tiles.
 #include "cmve_internal.h"
 
 namespace cmve {
@@ -22,8 +26,7 @@ typedef short s16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int PLANE_BYTES = BM * BK * 2;  // 16 KiB
+constexpr int BK = 64;
 constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2;
 constexpr int CAND_LDS = 1024;  // per-block undecided-pair buffer (one global atomic per block)
 
@@ -36,13 +39,13 @@ struct SimArgs {
   int nq, ng;
   int nblk_m, nblk_n;
   int nk;
-  // linear epilogue: v = acc + bias; relu; + resid; v * bn_scale + bn_shift
+  // linear epilogue: v = acc + bias; act; + resid; v * bn_scale + bn_shift
   const float* bias;
   const float* bn_scale;
   const float* bn_shift;
   const float* resid;
   int64_t ldr;
-  int relu;
+  int relu;  // activation: 0 none, 1 ReLU, 2 QuickGELU, 3 sigmoid
   // store
   void* out;
   int64_t ldo;
@@ -74,16 +77,20 @@ __device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, i
   bn = group * GN + (within - bm * gn);
 }
 
-// issue this wave's share (4 x 1 KiB) of one 128 x 64 bf16 plane
+// issue this wave's share of one ROWS x 64 (bf16/fp16) plane: ROWS/8 wave-instructions of 1 KiB
+template <int ROWS, int NW>
 __device__ __forceinline__ void stage_plane(const uint16_t* __restrict__ src, int64_t ldk, int row0, int k0,
                                             char* lds_plane, int wave, int lane) {
+  constexpr int PER_WAVE = ROWS / 8 / NW;
+  static_assert(PER_WAVE * 8 * NW == ROWS, "plane rows must split evenly over the waves");
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int r = (wave * 4 + it) * 8 + (lane >> 3);
+  for (int it = 0; it < PER_WAVE; ++it) {
+    const int chunk = wave * PER_WAVE + it;
+    const int r = chunk * 8 + (lane >> 3);
     const int c = lane & 7;
     const int gc = c ^ (r & 7);
     const uint16_t* g = src + (int64_t)(row0 + r) * ldk + k0 + gc * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void_t*)(lds_plane + (wave * 4 + it) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void_t*)(lds_plane + chunk * 1024), 16, 0, 0);
   }
 }
 
@@ -91,6 +98,15 @@ __device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chu
   // row & 7 == lane & 7 for every fragment row this kernel reads
   return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
+
+// ---- ring geometry (G256): K step 32, 64-B LDS rows, 4 slots, 3 stages in flight ----
+// A 64-B row holds 4 16-B chunks.  ds_read_b128 serves 4 lane groups of 16
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63}); fragment
+// lane l reads row (l & 15), chunk (l >> 4), i.e. 16-B bank slot (row*4 + chunk') mod 16.  The
+// chunk permutation chunk' = chunk ^ SWZ32[(row >> 2) & 3] with SWZ32 = {0, 2, 3, 1} maps every
+// group onto 16 distinct slots (checked by hand for all 4 groups): conflict-free.
+constexpr int BK32 = 32, RING = 4, AHEAD = 3;
+__device__ __forceinline__ int swz32(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
 template <int MODE>
 __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
@@ -102,97 +118,225 @@ __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
                                                    c, 0, 0, 0);
 }
 
-template <int MODE, int EPI>
-__global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NPLANE = (MODE == CMVE_SIM_BF16X3) ? 4 : 2;
-  constexpr int STAGE_BYTES = NPLANE * PLANE_BYTES;
+template <int WM, int WN, int TM>
+struct Geo {
+  static constexpr int TN = 4;
+  static constexpr int NW = WM * WN;
+  static constexpr int NT = NW * 64;
+  static constexpr int BM = WM * TM * 16;
+  static constexpr int BN = WN * TN * 16;
+};
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+template <int MODE, int BM, int BN>
+constexpr size_t stage_bytes() {
+  return (size_t)((MODE == CMVE_SIM_BF16X3) ? 2 : 1) * (BM + BN) * BK * 2;
+}
+
+template <int MODE, int BM, int BN, bool RINGED>
+constexpr size_t mainloop_lds() {
+  return RINGED ? (size_t)RING * (BM + BN) * BK32 * 2 : 2 * stage_bytes<MODE, BM, BN>();
+}
+
+template <int MODE, int EPI, int WM, int WN, int TM, bool RINGED>
+__global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
+  using G = Geo<WM, WN, TM>;
+  constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN>();
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static_assert(!RINGED || MODE != CMVE_SIM_BF16X3, "the ring path stages one plane per operand");
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
+  const int wr = wave / WN, wc = wave % WN;
   int bm, bn;
   tile_of_block(blockIdx.x, a.nblk_m, a.nblk_n, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
 
-  int* lds_rc = (int*)(smem + 2 * STAGE_BYTES);
+  // epilogue scratch after the staging buffers (one dynamic LDS object only)
+  int* lds_rc = (int*)(smem + mainloop_lds<MODE, BM, BN, RINGED>());
   int* lds_cc = lds_rc + BM;
   unsigned long long* lds_cand = (unsigned long long*)(lds_cc + BN);
   unsigned* lds_ncand = (unsigned*)(lds_cand + CAND_LDS);
+  unsigned long long* lds_cand_base = (unsigned long long*)(lds_ncand + 2);
   if (EPI == EPI_RANK) {
-    lds_rc[tid] = 0;  // 256 ints: 128 row + 128 col counters
+    for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
     if (tid == 0) *lds_ncand = 0u;
   }
 
   auto stage = [&](int t, int s) {
+#ifdef CMVE_DBG_NOLOAD
+    return;
+#endif
     char* base = smem + s * STAGE_BYTES;
     const int k0 = t * BK;
-    stage_plane(a.qhi, a.ldk, m0, k0, base, wave, lane);
-    stage_plane(a.ghi, a.ldk, n0, k0, base + PLANE_BYTES, wave, lane);
+    stage_plane<BM, NW>(a.qhi, a.ldk, m0, k0, base, wave, lane);
+    stage_plane<BN, NW>(a.ghi, a.ldk, n0, k0, base + A_BYTES, wave, lane);
     if (MODE == CMVE_SIM_BF16X3) {
-      stage_plane(a.qlo, a.ldk, m0, k0, base + 2 * PLANE_BYTES, wave, lane);
-      stage_plane(a.glo, a.ldk, n0, k0, base + 3 * PLANE_BYTES, wave, lane);
+      stage_plane<BM, NW>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, wave, lane);
+      stage_plane<BN, NW>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, wave, lane);
     }
   };
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  const int frow = lane & 15;
+  if constexpr (RINGED) {
+    // buffer_load ... lds: descriptor per operand block (base = first row of the block tile),
+    // one per-lane voffset shared by every piece (row (lane>>2) of a 16-row piece, swizzled
+    // chunk), the piece row and the K offset in the scalar soffset, the LDS target in M0.
+    constexpr int SLOT = (BM + BN) * BK32 * 2, A32 = BM * BK32 * 2;
+    constexpr int PA = BM / 16 / NW, PB = BN / 16 / NW;  // 16-row pieces per wave per plane
+    static_assert(PA * 16 * NW == BM && PB * 16 * NW == BN, "pieces must split evenly");
+    const int ldk_b = (int)(a.ldk * 2);
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.qhi + (int64_t)m0 * a.ldk), 0, BM * ldk_b, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.ghi + (int64_t)n0 * a.ldk), 0, BN * ldk_b, 0x00020000);
+    const int prow = lane >> 2;
+    const int voff = prow * ldk_b + (((lane & 3) ^ swz32(prow)) << 4);
+    auto stage32 = [&](int t, int s) {
+#ifdef CMVE_DBG_NOLOAD  // diagnostic build only: MFMA + LDS-read ceiling (results are garbage)
+      return;
+#endif
+      char* base = smem + s * SLOT;
+      const int kb = t * (BK32 * 2);
+#pragma unroll
+      for (int it = 0; it < PA; ++it) {
+        const int piece = wave * PA + it;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void_t*)(base + piece * 1024), 16, voff,
+                                                 piece * 16 * ldk_b + kb, 0, 0);
+      }
+#pragma unroll
+      for (int it = 0; it < PB; ++it) {
+        const int piece = wave * PB + it;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void_t*)(base + A32 + piece * 1024), 16, voff,
+                                                 piece * 16 * ldk_b + kb, 0, 0);
+      }
+    };
+    constexpr int LPS = PA + PB;  // loads per stage per lane (vmcnt units)
+    const int nk = a.nk * (BK / BK32);
+    // fragment read address inside a plane: row frow of each 16-row tile, chunk (lane >> 4)
+    const int fo = frow * 64 + (((lane >> 4) ^ swz32(frow)) << 4);
+    const int aoff = wr * (TM * 16) * 64 + fo, boff = A32 + wc * (TN * 16) * 64 + fo;
+#pragma unroll
+    for (int p = 0; p < AHEAD; ++p)
+      if (p < nk) stage32(p, p);
+    for (int t = 0; t < nk; ++t) {
+      // stage t landed for THIS wave once at most the later stages' loads are outstanding;
+      // the barrier then makes every wave's pieces of stage t visible, and proves every wave
+      // finished reading slot (t-1)&3, which the refill below overwrites
+      const int later = min(nk - 1 - t, AHEAD - 1);
+      if (later >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPS) : "memory");
+      else if (later == 1)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (t + AHEAD < nk) stage32(t + AHEAD, (t + AHEAD) & (RING - 1));
+      const char* base = smem + (t & (RING - 1)) * SLOT;
+      s16x8_t fa[TM], fb[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = *(const s16x8_t*)(base + boff + j * 1024);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *(const s16x8_t*)(base + aoff + i * 1024);
+#ifdef CMVE_DBG_NOMFMA  // diagnostic build only: staging + LDS-read floor (results are garbage)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+#else
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+#endif
+    }
+    __syncthreads();  // epilogue LDS scratch lives past the ring; keep the block in step
+  } else {
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  const int frow = lane & 15;
   for (int t = 0; t < a.nk; ++t) {
     if (t + 1 < a.nk) stage(t + 1, (t + 1) & 1);
     const char* base = smem + (t & 1) * STAGE_BYTES;
     const char* pA = base;
-    const char* pB = base + PLANE_BYTES;
+    const char* pB = base + A_BYTES;
+    // all fragments of this K step first (the compiler's counted lgkmcnt waits let the first
+    // MFMAs start on the first fragments), then ONE MFMA cluster: no LDS round trip inside it
+    s16x8_t fa[2][TM], fb[2][TN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
-      s16x8_t fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag(pA, wr * 64 + i * 16 + frow, chunk);
+      for (int j = 0; j < TN; ++j) fb[ks][j] = read_frag(pB, wc * (TN * 16) + j * 16 + frow, chunk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag(pB, wc * 64 + j * 16 + frow, chunk);
-      if (MODE == CMVE_SIM_BF16X3) {
-        const char* pAl = base + 2 * PLANE_BYTES;
-        const char* pBl = base + 3 * PLANE_BYTES;
-        s16x8_t la[4], lb[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) la[i] = read_frag(pAl, wr * 64 + i * 16 + frow, chunk);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) lb[j] = read_frag(pBl, wc * 64 + j * 16 + frow, chunk);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            acc[i][j] = mfma<MODE>(la[i], fb[j], acc[i][j]);
-            acc[i][j] = mfma<MODE>(fa[i], lb[j], acc[i][j]);
-          }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = mfma<MODE>(fa[i], fb[j], acc[i][j]);
+      for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag(pA, wr * (TM * 16) + i * 16 + frow, chunk);
     }
+    if constexpr (MODE == CMVE_SIM_BF16X3) {
+      const char* pAl = base + A_BYTES + B_BYTES;
+      const char* pBl = base + 2 * A_BYTES + B_BYTES;
+      s16x8_t la[2][TM], lb[2][TN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) la[ks][i] = read_frag(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) lb[ks][j] = read_frag(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = mfma<MODE>(la[ks][i], fb[ks][j], acc[i][j]);
+            acc[i][j] = mfma<MODE>(fa[ks][i], lb[ks][j], acc[i][j]);
+          }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#ifdef CMVE_DBG_NOMFMA
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[ks][i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[ks][j]));
+    }
+#else
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  }
 
   // ---------------- epilogues ----------------
-  // accumulator element (i, j, r): row = m0 + wr*64 + i*16 + (lane>>4)*4 + r, col = n0 + wc*64 + j*16 + (lane&15)
-  const int rbase = m0 + wr * 64 + (lane >> 4) * 4;
-  const int cbase = n0 + wc * 64 + (lane & 15);
+  // accumulator element (i, j, r): row = m0 + wr*TM*16 + i*16 + (lane>>4)*4 + r,
+  //                                col = n0 + wc*TN*16 + j*16 + (lane&15)
+  const int rbase = m0 + wr * (TM * 16) + (lane >> 4) * 4;
+  const int cbase = n0 + wc * (TN * 16) + (lane & 15);
 
   if constexpr (EPI == EPI_LINEAR) {
-    float bj[4], sj[4], hj[4];
+    float bj[TN], sj[TN], hj[TN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TN; ++j) {
       const int col = cbase + j * 16;
       const bool ok = col < a.ng;
       bj[j] = (a.bias && ok) ? a.bias[col] : 0.f;
@@ -200,19 +344,19 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
       hj[j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + i * 16 + r;
         if (row >= a.nq) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TN; ++j) {
           const int col = cbase + j * 16;
           if (col >= a.ng) continue;
           float v = acc[i][j][r] + bj[j];
-          if (a.relu == 1) v = fmaxf(v, 0.f);                                   // ReLU
-          else if (a.relu == 2) v = v / (1.f + expf(-1.702f * v));            // QuickGELU x*sigmoid(1.702x)
-          else if (a.relu == 3) v = 1.f / (1.f + expf(-v));                   // Sigmoid
+          if (a.relu == 1) v = fmaxf(v, 0.f);                         // ReLU
+          else if (a.relu == 2) v = v / (1.f + expf(-1.702f * v));  // QuickGELU x*sigmoid(1.702x)
+          else if (a.relu == 3) v = 1.f / (1.f + expf(-v));         // Sigmoid
           if (a.resid) v = a.resid[(int64_t)row * a.ldr + col] + v;
           if (a.bn_scale) v = v * sj[j] + hj[j];
           ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
@@ -220,13 +364,13 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
       }
   } else if constexpr (EPI == EPI_STORE) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + i * 16 + r;
         if (row >= a.nq) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TN; ++j) {
           const int col = cbase + j * 16;
           if (col >= a.ng) continue;
           const float v = a.alpha * acc[i][j][r] + a.beta;
@@ -237,42 +381,40 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
         }
       }
   } else {
-    // thresholds (+inf disables a direction / a padded row or column)
-    f32x4_t rhi[4], rlo[4];
-    float chi[4], clo[4];
+    // thresholds; a disabled direction gets NaN, which no comparison passes (not even s = +inf)
+    float chi[TN], clo[TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (a.row_hi) {
-        rhi[i] = *(const f32x4_t*)(a.row_hi + rbase + i * 16);
-        rlo[i] = *(const f32x4_t*)(a.row_lo + rbase + i * 16);
-      } else {
-        rhi[i] = f32x4_t{INFINITY, INFINITY, INFINITY, INFINITY};
-        rlo[i] = rhi[i];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      chi[j] = a.col_hi ? a.col_hi[cbase + j * 16] : INFINITY;
-      clo[j] = a.col_lo ? a.col_lo[cbase + j * 16] : INFINITY;
+    for (int j = 0; j < TN; ++j) {
+      chi[j] = a.col_hi ? a.col_hi[cbase + j * 16] : __builtin_nanf("");
+      clo[j] = a.col_lo ? a.col_lo[cbase + j * 16] : __builtin_nanf("");
     }
     const bool padded = (m0 + BM > a.nq) || (n0 + BN > a.ng);
-    uint32_t rc_pack[4] = {0u, 0u, 0u, 0u};  // byte r of rc_pack[i]: count for row (i, r)
-    uint32_t cc_pack = 0u;                    // byte j: count for column j
+    uint32_t cc_pack = 0u;  // byte j: count for column j (<= 4*TM per lane, <= 16*TM after the reduce)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i) {
+      f32x4_t rhi, rlo;
+      if (a.row_hi) {
+        rhi = *(const f32x4_t*)(a.row_hi + rbase + i * 16);
+        rlo = *(const f32x4_t*)(a.row_lo + rbase + i * 16);
+      } else {
+        const float qnan = __builtin_nanf("");
+        rhi = f32x4_t{qnan, qnan, qnan, qnan};
+        rlo = rhi;
+      }
+      uint32_t rc_pack = 0u;  // byte r: count for row (i, r) over this lane's TN columns
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float s = acc[i][j][r];
           const int row = rbase + i * 16 + r;
           const int col = cbase + j * 16;
           if (padded && (row >= a.nq || col >= a.ng)) s = -INFINITY;
-          const bool br = s > rhi[i][r];
+          const bool br = s > rhi[r];
           const bool bc = s > chi[j];
-          rc_pack[i] += (uint32_t)br << (8 * r);
+          rc_pack += (uint32_t)br << (8 * r);
           cc_pack += (uint32_t)bc << (8 * j);
-          const uint32_t flags = (uint32_t)((s >= rlo[i][r]) & !br) | ((uint32_t)((s >= clo[j]) & !bc) << 1);
+          const uint32_t flags = (uint32_t)((s >= rlo[r]) & !br) | ((uint32_t)((s >= clo[j]) & !bc) << 1);
           if (flags) {
             const unsigned long long packed =
                 (unsigned long long)row | ((unsigned long long)col << 31) | ((unsigned long long)flags << 62);
@@ -285,75 +427,89 @@ __global__ __launch_bounds__(256, 2) void sim_kernel(SimArgs a) {
             }
           }
         }
-    // rows: reduce over the 16 lanes that share (lane >> 4); bytes stay <= 64
+      // rows: reduce over the 16 lanes that share (lane >> 4); bytes stay <= 64
+      rc_pack += __shfl_xor(rc_pack, 1, 64);
+      rc_pack += __shfl_xor(rc_pack, 2, 64);
+      rc_pack += __shfl_xor(rc_pack, 4, 64);
+      rc_pack += __shfl_xor(rc_pack, 8, 64);
+      if ((lane & 15) == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint32_t v = rc_pack[i];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      rc_pack[i] = v;
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t c = (rc_pack >> (8 * r)) & 0xffu;
+          if (c) atomicAdd(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
+        }
+      }
     }
     cc_pack += __shfl_xor(cc_pack, 16, 64);
     cc_pack += __shfl_xor(cc_pack, 32, 64);
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t c = (rc_pack[i] >> (8 * r)) & 0xffu;
-          if (c) atomicAdd(&lds_rc[wr * 64 + i * 16 + (lane >> 4) * 4 + r], (int)c);
-        }
-    }
     if (lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TN; ++j) {
         const uint32_t c = (cc_pack >> (8 * j)) & 0xffu;
-        if (c) atomicAdd(&lds_cc[wc * 64 + j * 16 + lane], (int)c);
+        if (c) atomicAdd(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
       }
     }
     __syncthreads();
     // flush the block's undecided pairs with ONE global atomic
-    __shared__ unsigned long long cand_base;
     const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
-    if (tid == 0 && nlds) cand_base = atomicAdd(a.cand_count, (unsigned long long)nlds);
+    if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.cand_count, (unsigned long long)nlds);
     __syncthreads();
-    for (unsigned t = tid; t < nlds; t += 256) {
-      const unsigned long long slot = cand_base + t;
+    for (unsigned t = tid; t < nlds; t += NT) {
+      const unsigned long long slot = *lds_cand_base + t;
       if ((long long)slot < a.cand_cap) a.cand[slot] = lds_cand[t];
     }
-    if (tid < BM) {
-      const int c = lds_rc[tid];
-      if (c && a.row_cnt && m0 + tid < a.nq) atomicAdd(&a.row_cnt[m0 + tid], c);
-    } else {
-      const int c = lds_cc[tid - BM];
-      if (c && a.col_cnt && n0 + tid - BM < a.ng) atomicAdd(&a.col_cnt[n0 + tid - BM], c);
+    for (int t = tid; t < BM + BN; t += NT) {
+      const int c = lds_rc[t];
+      if (!c) continue;
+      if (t < BM) {
+        if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
+      } else {
+        if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
+      }
     }
   }
 }
 
-template <int MODE, int EPI>
-static int launch_sim(const SimArgs& a, hipStream_t stream) {
-  constexpr int NPLANE = (MODE == CMVE_SIM_BF16X3) ? 4 : 2;
-  const size_t lds = 2 * (size_t)NPLANE * PLANE_BYTES +
-                     (EPI == EPI_RANK ? 2 * 128 * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 : 0);
+template <int MODE, int EPI, int WM, int WN, int TM, bool RINGED>
+static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
+  using G = Geo<WM, WN, TM>;
+  const size_t lds = mainloop_lds<MODE, G::BM, G::BN, RINGED>() +
+                     (EPI == EPI_RANK ? (G::BM + G::BN) * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 : 0);
   static bool attr_done = false;
   if (!attr_done) {
-    CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)lds));
+    CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, RINGED>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_done = true;
   }
+  a.nblk_m = (int)(nq_pad / G::BM);
+  a.nblk_n = (int)(ng_pad / G::BN);
   const unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
-  hipLaunchKernelGGL((sim_kernel<MODE, EPI>), dim3(nblocks), dim3(256), lds, stream, a);
+  hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, RINGED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
   return check_launch("sim_kernel");
+}
+
+// G256 (ring pipeline) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
+// tiles; else G128 (2-stage).  CMVE_SIM_GEO=128 forces G128 (kernel benchmarking only).
+template <int MODE, int EPI>
+static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
+  static const int force = [] {
+    const char* e = getenv("CMVE_SIM_GEO");
+    return e ? atoi(e) : 0;
+  }();
+  if constexpr (MODE != CMVE_SIM_BF16X3) {
+    if (force != 128 && nq_pad % 256 == 0 && ng_pad % 256 == 0 && (nq_pad / 256) * (ng_pad / 256) >= 512) {
+      if (force == 2562) return launch_geo<MODE, EPI, 2, 4, 8, false>(a, nq_pad, ng_pad, stream);  // 2-stage BK64
+      return launch_geo<MODE, EPI, 2, 4, 8, true>(a, nq_pad, ng_pad, stream);
+    }
+  }
+  return launch_geo<MODE, EPI, 2, 2, 4, false>(a, nq_pad, ng_pad, stream);
 }
 
 static int validate_pair(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, const char* fn) {
   CMVE_REQUIRE(q && g, "%s: NULL rows", fn);
   CMVE_REQUIRE(q->d == g->d && q->d_pad == g->d_pad, "%s: dimension mismatch (%lld vs %lld)", fn, (long long)q->d,
                (long long)g->d);
-  CMVE_REQUIRE(q->n_pad % BM == 0 && g->n_pad % BN == 0 && q->d_pad % BK == 0, "%s: sets not packed/padded", fn);
+  CMVE_REQUIRE(q->n_pad % 128 == 0 && g->n_pad % 128 == 0 && q->d_pad % BK == 0, "%s: sets not packed/padded", fn);
   CMVE_REQUIRE(q->n <= q->n_pad && g->n <= g->n_pad, "%s: n > n_pad", fn);
   CMVE_REQUIRE(q->n < (1ll << 31) && g->n < (1ll << 31), "%s: set too large for int32 indices", fn);
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16, "%s: unknown mode %d", fn,
@@ -373,10 +529,15 @@ static SimArgs make_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mod
   a.ldk = q->d_pad;
   a.nq = (int)q->n;
   a.ng = (int)g->n;
-  a.nblk_m = (int)(q->n_pad / BM);
-  a.nblk_n = (int)(g->n_pad / BN);
   a.nk = (int)(q->d_pad / BK);
   return a;
+}
+
+template <int EPI>
+static int dispatch(const SimArgs& a, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, hipStream_t s) {
+  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI>(a, q->n_pad, g->n_pad, s);
+  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI>(a, q->n_pad, g->n_pad, s);
+  return launch_sim<CMVE_SIM_BF16X3, EPI>(a, q->n_pad, g->n_pad, s);
 }
 
 }  // namespace cmve
@@ -397,9 +558,7 @@ extern "C" int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_
   a.alpha = alpha;
   a.beta = beta;
   a.out_f64 = out_dtype == CMVE_F64;
-  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_STORE>(a, h->stream);
-  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_STORE>(a, h->stream);
-  return launch_sim<CMVE_SIM_BF16X3, EPI_STORE>(a, h->stream);
+  return dispatch<EPI_STORE>(a, q, g, mode, h->stream);
 }
 
 // defined in rank.hip
@@ -448,9 +607,7 @@ extern "C" int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_
   if (dirs & CMVE_DIR_ROW) CMVE_HIP(hipMemsetAsync(row_cnt, 0, sizeof(int32_t) * q->n_pad, h->stream));
   if (dirs & CMVE_DIR_COL) CMVE_HIP(hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * g->n_pad, h->stream));
   if (q->n == 0 || g->n == 0) return CMVE_OK;
-  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_RANK>(a, h->stream);
-  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_RANK>(a, h->stream);
-  return launch_sim<CMVE_SIM_BF16X3, EPI_RANK>(a, h->stream);
+  return dispatch<EPI_RANK>(a, q, g, mode, h->stream);
 }
 
 extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
@@ -487,6 +644,7 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
   CMVE_REQUIRE(out && ldo >= w->n, "cmve_linear: bad output");
   CMVE_REQUIRE((bn_scale == nullptr) == (bn_shift == nullptr), "cmve_linear: bn_scale and bn_shift go together");
   CMVE_REQUIRE(!resid || ldr >= w->n, "cmve_linear: bad residual leading dimension");
+  CMVE_REQUIRE(relu >= 0 && relu <= 3, "cmve_linear: unknown activation %d", relu);
   if (x->n == 0 || w->n == 0) return CMVE_OK;
   SimArgs a = make_args(x, w, mode);
   a.out = out;
@@ -497,7 +655,5 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
   a.resid = resid;
   a.ldr = ldr;
   a.relu = relu;
-  if (mode == CMVE_SIM_BF16) return launch_sim<CMVE_SIM_BF16, EPI_LINEAR>(a, h->stream);
-  if (mode == CMVE_SIM_F16) return launch_sim<CMVE_SIM_F16, EPI_LINEAR>(a, h->stream);
-  return launch_sim<CMVE_SIM_BF16X3, EPI_LINEAR>(a, h->stream);
+  return dispatch<EPI_LINEAR>(a, x, w, mode, h->stream);
 }

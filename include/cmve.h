@@ -50,7 +50,7 @@ enum cmve_rank_dir { CMVE_DIR_ROW = 1, CMVE_DIR_COL = 2 };
 
 /* Tile geometry of the packed planes: rows padded to CMVE_ROW_ALIGN,
  * dimension padded to CMVE_DIM_ALIGN (zero fill). */
-#define CMVE_ROW_ALIGN 128
+#define CMVE_ROW_ALIGN 256
 #define CMVE_DIM_ALIGN 64
 
 /*

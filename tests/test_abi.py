@@ -35,7 +35,7 @@ def test_host_only_entry_points():
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)
     assert _lib.lib.cmve_pack_size(1, 100, C.byref(n_pad), C.byref(d_pad)) == 0
-    assert (n_pad.value, d_pad.value) == (128, 128)
+    assert (n_pad.value, d_pad.value) == (256, 128)
     assert _lib.lib.cmve_pack_size(-1, 100, C.byref(n_pad), C.byref(d_pad)) < 0
     assert b"pack_size" in _lib.lib.cmve_last_error()
 

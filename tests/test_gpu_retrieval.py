@@ -29,7 +29,7 @@ def test_pack_normalises_and_bounds_hold(torch_cuda):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((300, 100)) * rng.uniform(0.1, 10, (300, 1))
     rs = engine.RowSet(x, eps=0.0, with_lo=True)
-    assert (rs.n_pad, rs.d_pad) == (384, 128)
+    assert (rs.n_pad, rs.d_pad) == (512, 128)
     xhat = R.l2norm(x)
     hi = rs.hi[:300, :100].cpu().numpy().view(np.uint16).astype(np.uint32) << 16
     lo = rs.lo[:300, :100].cpu().numpy().view(np.uint16).astype(np.uint32) << 16

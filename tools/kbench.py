@@ -13,7 +13,7 @@ import torch  # noqa: E402
 from cmve import engine, _lib  # noqa: E402
 
 
-def timed(fn, reps=5):
+def timed(fn, reps=int(os.environ.get("REPS", 5))):
     fn()
     torch.cuda.synchronize()
     evs = []
@@ -41,7 +41,10 @@ def main():
     ws = engine.RankWorkspace(dev, cap=1 << 25)
     inf = torch.full((Q.n_pad,), float("inf"), dtype=torch.float32, device=dev)
     flops = 2.0 * nq * ng * d
+    modes = os.environ.get("MODES", "BF16,F16,BF16X3").split(",")
     for name, mode in (("BF16", _lib.SIM_BF16), ("F16", _lib.SIM_F16), ("BF16X3", _lib.SIM_BF16X3)):
+        if name not in modes:
+            continue
         sgt, hi, lo = engine.gt_thresholds(Q, G, off, idx, mode)
         cnt = torch.empty(Q.n_pad, dtype=torch.int32, device=dev)
         h = engine.handle(dev)
@@ -58,7 +61,7 @@ def main():
         t_plain = timed(lambda: mfma(inf, inf))
         t_rank = timed(lambda: mfma(hi, lo))
         ncand = int(ws.count.item())
-        t_fix = timed(fix)
+        t_fix = timed(fix) if not os.environ.get("KB_NOFIX") else float("nan")  # diagnostic builds: garbage pairs
         E = float((hi - lo)[:nq].double().mean().item()) / 2
         mult = 3 if mode == _lib.SIM_BF16X3 else 1
         print(json.dumps({"mode": name, "gemm_only_ms": t_plain, "rank_mfma_ms": t_rank, "fixup_ms": t_fix,
