@@ -99,15 +99,6 @@ __device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chu
   return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
 
-// ---- ring geometry (G256): K step 32, 64-B LDS rows, 4 slots, 3 stages in flight ----
-// A 64-B row holds 4 16-B chunks.  ds_read_b128 serves 4 lane groups of 16
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63}); fragment
-// lane l reads row (l & 15), chunk (l >> 4), i.e. 16-B bank slot (row*4 + chunk') mod 16.  The
-// chunk permutation chunk' = chunk ^ SWZ32[(row >> 2) & 3] with SWZ32 = {0, 2, 3, 1} maps every
-// group onto 16 distinct slots (checked by hand for all 4 groups): conflict-free.
-constexpr int BK32 = 32, RING = 4, AHEAD = 3;
-__device__ __forceinline__ int swz32(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
-
 template <int MODE>
 __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
   if constexpr (MODE == CMVE_SIM_F16)
@@ -132,19 +123,14 @@ constexpr size_t stage_bytes() {
   return (size_t)((MODE == CMVE_SIM_BF16X3) ? 2 : 1) * (BM + BN) * BK * 2;
 }
 
-template <int MODE, int BM, int BN, bool RINGED>
-constexpr size_t mainloop_lds() {
-  return RINGED ? (size_t)RING * (BM + BN) * BK32 * 2 : 2 * stage_bytes<MODE, BM, BN>();
-}
-
-template <int MODE, int EPI, int WM, int WN, int TM, bool RINGED>
+template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN>();
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  static_assert(!RINGED || MODE != CMVE_SIM_BF16X3, "the ring path stages one plane per operand");
+  static_assert(!PHASED || MODE != CMVE_SIM_BF16X3, "the phased path stages one plane per operand");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
@@ -154,7 +140,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   const int m0 = bm * BM, n0 = bn * BN;
 
   // epilogue scratch after the staging buffers (one dynamic LDS object only)
-  int* lds_rc = (int*)(smem + mainloop_lds<MODE, BM, BN, RINGED>());
+  int* lds_rc = (int*)(smem + 2 * STAGE_BYTES);
   int* lds_cc = lds_rc + BM;
   unsigned long long* lds_cand = (unsigned long long*)(lds_cc + BN);
   unsigned* lds_ncand = (unsigned*)(lds_cand + CAND_LDS);
@@ -185,80 +171,128 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15;
-  if constexpr (RINGED) {
-    // buffer_load ... lds: descriptor per operand block (base = first row of the block tile),
-    // one per-lane voffset shared by every piece (row (lane>>2) of a 16-row piece, swizzled
-    // chunk), the piece row and the K offset in the scalar soffset, the LDS target in M0.
-    constexpr int SLOT = (BM + BN) * BK32 * 2, A32 = BM * BK32 * 2;
-    constexpr int PA = BM / 16 / NW, PB = BN / 16 / NW;  // 16-row pieces per wave per plane
-    static_assert(PA * 16 * NW == BM && PB * 16 * NW == BN, "pieces must split evenly");
+  if constexpr (PHASED) {
+    // ---- G256 phased schedule (2 buffers of BK=64, 4 phases per K-tile, 2 staggered groups) ----
+    // phase = { ds_read subtile, [LDS-DMA issue], [counted vmcnt], s_barrier,
+    //           16 MFMAs (one 64x32 quadrant of the wave's 128x64 tile, K=64), s_barrier }.
+    // Group 1 (waves 4-7, wr = 1) runs one barrier behind group 0, so on every SIMD (waves w and
+    // w+4) one wave issues MFMAs while the other reads LDS / issues loads.
+    //   K-tile t (buffer t&1):   r=1 reads A(qm0)+B(qn0), MFMA Q00;  r=2 reads B(qn1), Q01;
+    //                            r=3 reads A(qm1), Q11;               r=4 no reads, Q10.
+    //   loads: A(t+1) at r=1 (its buffer's A was last read 2 phases earlier, r=3 of t-1),
+    //          B(t+2) at r=4 (this buffer's B was last read at r=2); r=4 waits for K-tile t+1
+    //          with only B(t+2) younger: vmcnt(4) -- 3 to 4 phases for every load to land.
+    // RAW: a wait before phase p's first barrier covers reads from phase p+1 on, for both groups;
+    // WAR: a buffer is restaged >= 2 phases after its last ds_read (cdna_hip_programming.md Sec.5).
+    static_assert(BM == 256 && BN == 256 && TM == 8 && TN == 4 && NW == 8, "phased path is the 256x256 geometry");
     const int ldk_b = (int)(a.ldk * 2);
     const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.qhi + (int64_t)m0 * a.ldk), 0, BM * ldk_b, 0x00020000);
     const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.ghi + (int64_t)n0 * a.ldk), 0, BN * ldk_b, 0x00020000);
-    const int prow = lane >> 2;
-    const int voff = prow * ldk_b + (((lane & 3) ^ swz32(prow)) << 4);
-    auto stage32 = [&](int t, int s) {
+    // piece = 8 rows x 128 B (one wave-instruction, 1 KiB): lane l -> row l>>3, LDS chunk l&7,
+    // global chunk (l&7) ^ (row&7)
+    const int voff = (lane >> 3) * ldk_b + (((lane & 7) ^ (lane >> 3)) << 4);
+    auto stage_op = [&](const __amdgpu_buffer_rsrc_t& r, int t, int plane_off) {
 #ifdef CMVE_DBG_NOLOAD  // diagnostic build only: MFMA + LDS-read ceiling (results are garbage)
       return;
 #endif
-      char* base = smem + s * SLOT;
-      const int kb = t * (BK32 * 2);
+      char* dst = smem + (t & 1) * STAGE_BYTES + plane_off;
+      const int kb = t * (BK * 2);
 #pragma unroll
-      for (int it = 0; it < PA; ++it) {
-        const int piece = wave * PA + it;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void_t*)(base + piece * 1024), 16, voff,
-                                                 piece * 16 * ldk_b + kb, 0, 0);
-      }
-#pragma unroll
-      for (int it = 0; it < PB; ++it) {
-        const int piece = wave * PB + it;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void_t*)(base + A32 + piece * 1024), 16, voff,
-                                                 piece * 16 * ldk_b + kb, 0, 0);
+      for (int it = 0; it < 4; ++it) {  // 32 pieces per 256-row plane, 4 per wave
+        const int piece = wave * 4 + it;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(dst + piece * 1024), 16, voff,
+                                                 piece * 8 * ldk_b + kb, 0, 0);
       }
     };
-    constexpr int LPS = PA + PB;  // loads per stage per lane (vmcnt units)
-    const int nk = a.nk * (BK / BK32);
-    // fragment read address inside a plane: row frow of each 16-row tile, chunk (lane >> 4)
-    const int fo = frow * 64 + (((lane >> 4) ^ swz32(frow)) << 4);
-    const int aoff = wr * (TM * 16) * 64 + fo, boff = A32 + wc * (TN * 16) * 64 + fo;
+    const int nk = a.nk;
+    // fragment address: row (tile row + frow), chunk (ks*4 + lane>>4) ^ (row & 7) with row&7 == lane&7
+    const int c0 = ((0 + (lane >> 4)) ^ (lane & 7)) << 4, c1 = ((4 + (lane >> 4)) ^ (lane & 7)) << 4;
+    const int arow = (wr * 128 + frow) * 128, brow = A_BYTES + (wc * 64 + frow) * 128;
+    s16x8_t fa[4][2], fb0[2][2], fb1[2][2];
+    auto read_a = [&](const char* buf, int qm) {
 #pragma unroll
-    for (int p = 0; p < AHEAD; ++p)
-      if (p < nk) stage32(p, p);
-    for (int t = 0; t < nk; ++t) {
-      // stage t landed for THIS wave once at most the later stages' loads are outstanding;
-      // the barrier then makes every wave's pieces of stage t visible, and proves every wave
-      // finished reading slot (t-1)&3, which the refill below overwrites
-      const int later = min(nk - 1 - t, AHEAD - 1);
-      if (later >= 2)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(2 * LPS) : "memory");
-      else if (later == 1)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPS) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (t + AHEAD < nk) stage32(t + AHEAD, (t + AHEAD) & (RING - 1));
-      const char* base = smem + (t & (RING - 1)) * SLOT;
-      s16x8_t fa[TM], fb[TN];
+      for (int i = 0; i < 4; ++i) {
+        const char* p = buf + arow + (qm * 64 + i * 16) * 128;
+        fa[i][0] = *(const s16x8_t*)(p + c0);
+        fa[i][1] = *(const s16x8_t*)(p + c1);
+      }
+    };
+    auto read_b = [&](const char* buf, int qn, s16x8_t (&fb)[2][2]) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = *(const s16x8_t*)(base + boff + j * 1024);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = *(const s16x8_t*)(base + aoff + i * 1024);
+      for (int j = 0; j < 2; ++j) {
+        const char* p = buf + brow + (qn * 32 + j * 16) * 128;
+        fb[j][0] = *(const s16x8_t*)(p + c0);
+        fb[j][1] = *(const s16x8_t*)(p + c1);
+      }
+    };
+    auto quadrant = [&](int qm, int qn, const s16x8_t (&fb)[2][2]) {
 #ifdef CMVE_DBG_NOMFMA  // diagnostic build only: staging + LDS-read floor (results are garbage)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+      for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fa[i][0]), "v"(fa[i][1]));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+      for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(fb[j][0]), "v"(fb[j][1]));
 #else
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[i], fb[j], acc[i][j]);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qm * 4 + i][qn * 2 + j] = mfma<MODE>(fa[i][ks], fb[j][ks], acc[qm * 4 + i][qn * 2 + j]);
       __builtin_amdgcn_s_setprio(0);
 #endif
+    };
+#define CMVE_BAR()                                  \
+  __builtin_amdgcn_sched_barrier(0);                \
+  asm volatile("s_barrier" ::: "memory");           \
+  __builtin_amdgcn_sched_barrier(0)
+
+    // prologue: K-tile 0 (A, B) and B(1); wait for K-tile 0
+    stage_op(rA, 0, 0);
+    stage_op(rB, 0, A_BYTES);
+    if (nk > 1) {
+      stage_op(rB, 1, A_BYTES);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();  // epilogue LDS scratch lives past the ring; keep the block in step
+    CMVE_BAR();
+    if (wr == 1) { CMVE_BAR(); }  // stagger: group 1 runs one barrier behind
+    for (int t = 0; t < nk; ++t) {
+      const char* buf = smem + (t & 1) * STAGE_BYTES;
+      // r = 1
+      if (t + 1 < nk) stage_op(rA, t + 1, 0);
+      read_a(buf, 0);
+      read_b(buf, 0, fb0);
+      CMVE_BAR();
+      quadrant(0, 0, fb0);
+      CMVE_BAR();
+      // r = 2
+      read_b(buf, 1, fb1);
+      CMVE_BAR();
+      quadrant(0, 1, fb1);
+      CMVE_BAR();
+      // r = 3
+      read_a(buf, 1);
+      CMVE_BAR();
+      quadrant(1, 1, fb1);
+      CMVE_BAR();
+      // r = 4: restage B of this buffer with K-tile t+2; K-tile t+1 must have landed
+      if (t + 2 < nk) {
+        stage_op(rB, t + 2, A_BYTES);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      CMVE_BAR();
+      quadrant(1, 0, fb0);
+      CMVE_BAR();
+    }
+    if (wr == 0) { CMVE_BAR(); }  // re-align the barrier counts of the two groups
+#undef CMVE_BAR
   } else {
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -470,26 +504,27 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   }
 }
 
-template <int MODE, int EPI, int WM, int WN, int TM, bool RINGED>
+template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = mainloop_lds<MODE, G::BM, G::BN, RINGED>() +
+  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN>() +
                      (EPI == EPI_RANK ? (G::BM + G::BN) * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 : 0);
   static bool attr_done = false;
   if (!attr_done) {
-    CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, RINGED>,
+    CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_done = true;
   }
   a.nblk_m = (int)(nq_pad / G::BM);
   a.nblk_n = (int)(ng_pad / G::BN);
   const unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
-  hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, RINGED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
+  hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, PHASED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
   return check_launch("sim_kernel");
 }
 
-// G256 (ring pipeline) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
-// tiles; else G128 (2-stage).  CMVE_SIM_GEO=128 forces G128 (kernel benchmarking only).
+// G256 (phased schedule) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
+// tiles; else G128 (2-stage).  CMVE_SIM_GEO=128 / 2562 force G128 / the 2-stage G256 loop
+// (kernel studies only).
 template <int MODE, int EPI>
 static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   static const int force = [] {
