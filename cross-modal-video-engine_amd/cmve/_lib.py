@@ -24,6 +24,7 @@ SIM_BF16, SIM_BF16X3, SIM_F16 = 0, 1, 2
 DIR_ROW, DIR_COL = 1, 2
 ROW_ALIGN, DIM_ALIGN = 256, 64
 TOPK_MAX = 2048
+MAX_CHUNKS = 16
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 
@@ -71,6 +72,9 @@ SIGNATURES = {
     "cmve_rank_mfma": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                                  _vp]),
     "cmve_rank_fixup": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "cmve_rank_count_overlap": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _i64, _vp, _i32]),
+    "cmve_overlap_mfma_ms": (C.c_int, [_vp, _P(_f32), _P(_i32)]),
     "cmve_rank_thresholds": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),

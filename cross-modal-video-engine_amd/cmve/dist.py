@@ -117,7 +117,7 @@ class ShardedGallery:
         return out
 
     def rank_queries(self, q_local: torch.Tensor, gt_csr, n_q: int, mode: int = _lib.SIM_F16, events=None,
-                     return_host: bool = True):
+                     return_host: bool = True, chunks: int = 1):
         """Global 1-based GT ranks of all gathered queries (t2v direction).
 
         q_local: this rank's [n_local, D] query embeddings (equal n_local on every rank);
@@ -129,15 +129,15 @@ class ShardedGallery:
         sgt, _, _ = engine.gt_thresholds(q, self.shard, off, idx, mode)
         sgt = merge_gt_scores(sgt, self.world)
         hi, lo = engine.rank_thresholds(q, self.shard, sgt, mode)
-        cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events)
+        cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events,
+                                          chunks=chunks)
         cnt = reduce_counts(cnt, self.world)
         ranks = ranks_from(cnt, sgt, n_q, self.n_global)
         if not return_host:
             return ranks
-        ncand = int(self.ws.count.item())
-        if ncand > self.ws.cap:  # overflow: grow and redo (correctness first)
-            self.ws.grow(ncand)
-            return self.rank_queries(q_local, gt_csr, n_q, mode, None, return_host)
+        if self.ws.overflowed():  # overflow: grow and redo (correctness first)
+            self.ws.grow()
+            return self.rank_queries(q_local, gt_csr, n_q, mode, None, return_host, chunks)
         return ranks.cpu().numpy().astype(np.int64)
 
     def topk(self, q_local: torch.Tensor, k: int, mode: int = _lib.SIM_F16):

@@ -175,19 +175,31 @@ def gt_thresholds(a: RowSet, b: RowSet, off: torch.Tensor, idx: torch.Tensor, mo
 
 
 class RankWorkspace:
-    """Reusable device buffers for rank_count (candidate list grows on overflow)."""
+    """Reusable device buffers for rank_count: the undecided-pair list (grown on overflow) and
+    one int64 pair counter per gallery chunk (cmve_rank_count_overlap)."""
 
     def __init__(self, device, cap: int = 1 << 20):
         self.device = device
         self.cand = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
-        self.count = torch.zeros(1, dtype=torch.int64, device=device)
+        self.count = torch.zeros(_lib.MAX_CHUNKS, dtype=torch.int64, device=device)
+        self.chunks = 1
 
     @property
     def cap(self):
         return self.cand.numel()
 
-    def grow(self, need: int):
-        self.cand = torch.empty(int(need * 1.25) + 1024, dtype=torch.int64, device=self.device)
+    def ncand(self) -> int:
+        """Undecided pairs of the last launch (synchronises)."""
+        return int(self.count[:self.chunks].sum().item())
+
+    def overflowed(self) -> bool:
+        """True if a chunk's list outgrew its share of the buffer (counts incomplete)."""
+        return bool((self.count[:self.chunks] > self.cap // self.chunks).any().item())
+
+    def grow(self, need: int = 0):
+        need = max(need, self.ncand())
+        self.cand = torch.empty(int(need * 1.25) * self.chunks + 1024 * self.chunks, dtype=torch.int64,
+                                device=self.device)
 
 
 def rank_thresholds(a: RowSet, b: RowSet, sgt: torch.Tensor, mode: int):
@@ -200,9 +212,12 @@ def rank_thresholds(a: RowSet, b: RowSet, sgt: torch.Tensor, mode: int):
 
 
 def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: Optional[RankWorkspace] = None,
-                      row_cnt=None, col_cnt=None, events=None):
+                      row_cnt=None, col_cnt=None, events=None, chunks: int = 1):
     """Enqueue the fused rank count (no sync).  row/col = (sgt, thr_hi, thr_lo) or None.
-    events = (start, mid, end) torch.cuda.Event triple recorded around the MFMA pass and the fix-up."""
+    chunks > 1: cmve_rank_count_overlap -- the gallery in `chunks` pieces, each piece's fp64
+    fix-up on the handle's auxiliary stream behind the next piece's MFMA pass.
+    events = (start, mid, end) torch.cuda.Event triple recorded around the MFMA pass and the
+    fix-up (with chunks > 1 the two overlap: mid is recorded with end)."""
     dirs = (_lib.DIR_ROW if row is not None else 0) | (_lib.DIR_COL if col is not None else 0)
     if row is not None and row_cnt is None:
         row_cnt = torch.empty(q.n_pad, dtype=torch.int32, device=q.device)
@@ -211,8 +226,19 @@ def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: O
     r = row if row is not None else (None, None, None)
     c = col if col is not None else (None, None, None)
     h = handle(q.device)
+    chunks = max(1, min(int(chunks), _lib.MAX_CHUNKS))
+    ws.chunks = chunks
     if events is not None:
         events[0].record()
+    if chunks > 1:
+        check(lib.cmve_rank_count_overlap(h, C.byref(q.desc), C.byref(g.desc), mode, dirs, _ptr(r[0]), _ptr(r[1]),
+                                          _ptr(r[2]), _ptr(c[0]), _ptr(c[1]), _ptr(c[2]), _ptr(row_cnt),
+                                          _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count), chunks),
+              "cmve_rank_count_overlap")
+        if events is not None:
+            events[1].record()
+            events[2].record()
+        return row_cnt, col_cnt
     check(lib.cmve_rank_mfma(h, C.byref(q.desc), C.byref(g.desc), mode, dirs, _ptr(r[1]), _ptr(r[2]), _ptr(c[1]),
                              _ptr(c[2]), _ptr(row_cnt), _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)),
           "cmve_rank_mfma")
@@ -226,7 +252,7 @@ def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: O
 
 
 def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int = _lib.SIM_F16,
-                   ws: Optional[RankWorkspace] = None):
+                   ws: Optional[RankWorkspace] = None, chunks: int = 1):
     """Exact GT ranks in both directions from ONE fused GEMM pass.
 
     row_gts[i]: GT indices into g for query row i (t2v); col_gts[j]: GT indices into q
@@ -248,9 +274,9 @@ def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int =
         coff, cidx = csr(col_gts, q.device)
         col = gt_thresholds(g, q, coff, cidx, mode)
     for _attempt in range(4):
-        rc, cc = rank_count_launch(q, g, mode, row, col, ws)
-        ncand = int(ws.count.item())  # synchronises
-        if ncand <= ws.cap:
+        rc, cc = rank_count_launch(q, g, mode, row, col, ws, chunks=chunks)
+        ncand = ws.ncand()  # synchronises
+        if not ws.overflowed():
             break
         ws.grow(ncand)
     else:

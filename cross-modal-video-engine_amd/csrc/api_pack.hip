@@ -34,13 +34,41 @@ int check_launch(const char* what) {
 // ---------------------------------------------------------------------------
 // K1: pack
 // ---------------------------------------------------------------------------
-template <typename T>
+// one element of a normalised row -> bf16 hi / bf16 lo / fp16 planes, with the squared residuals
+// of each representation accumulated in fp64 (the bounds are computed from the values STORED,
+// so the f16 conversion need not be correctly rounded from fp64: it goes through fp32, which the
+// hardware converts directly -- gfx950 has no fp64 -> fp16 instruction)
+struct PackAcc {
+  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
+};
+__device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h, uint16_t& l, uint16_t& f,
+                                          PackAcc& acc) {
+  const float xf = (float)xh;
+  if (want_f16) {
+    const _Float16 hf16 = (_Float16)xf;
+    const double r3 = xh - (double)hf16;
+    acc.e3 = fma(r3, r3, acc.e3);
+    f = __builtin_bit_cast(uint16_t, hf16);
+  }
+  h = f2bf(xf);
+  const float hf = bf2f(h);
+  l = f2bf(xf - hf);
+  const double r1 = xh - (double)hf;
+  const double r2 = r1 - (double)bf2f(l);
+  acc.e1 = fma(r1, r1, acc.e1);
+  acc.e2 = fma(r2, r2, acc.e2);
+}
+
+// One wave per row.  VEC: fp32 rows with d % 4 == 0 and 16-B aligned rows -- each lane moves 4
+// consecutive elements (16-B loads, 8-B plane stores); otherwise one element per lane step.
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ raw, int64_t ld, int64_t n,
                                                         int64_t d, int64_t n_pad, int64_t d_pad, double eps, int flags,
                                                         uint16_t* __restrict__ hi, uint16_t* __restrict__ lo,
                                                         uint16_t* __restrict__ h16, double* __restrict__ inv_norm,
                                                         float* __restrict__ err_hi, float* __restrict__ err_hilo,
                                                         float* __restrict__ err_h16, float* __restrict__ err_max) {
+  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_pad) return;
@@ -48,10 +76,11 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
   uint16_t* lrow = lo ? lo + row * d_pad : nullptr;
   uint16_t* frow = h16 ? h16 + row * d_pad : nullptr;
   if (row >= n) {  // padding rows: zero vectors, zero bounds
-    for (int64_t k = lane; k < d_pad; k += 64) {
-      hrow[k] = 0;
-      if (lrow) lrow[k] = 0;
-      if (frow) frow[k] = 0;
+    const u16x4 z = {0, 0, 0, 0};
+    for (int64_t k = lane * 4; k < d_pad; k += 256) {  // d_pad % 64 == 0
+      *(u16x4*)(hrow + k) = z;
+      if (lrow) *(u16x4*)(lrow + k) = z;
+      if (frow) *(u16x4*)(frow + k) = z;
     }
     if (lane == 0) {
       inv_norm[row] = 0.0;
@@ -63,43 +92,55 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
   }
   const T* x = raw + row * ld;
   double ss = 0.0;
-  for (int64_t k = lane; k < d; k += 64) {
-    double v = (double)x[k];
-    ss = fma(v, v, ss);
+  if constexpr (VEC) {
+    for (int64_t k = lane * 4; k < d; k += 256) {
+      const float4 v = *(const float4*)(x + k);
+      ss = fma((double)v.x, (double)v.x, ss);
+      ss = fma((double)v.y, (double)v.y, ss);
+      ss = fma((double)v.z, (double)v.z, ss);
+      ss = fma((double)v.w, (double)v.w, ss);
+    }
+  } else {
+    for (int64_t k = lane; k < d; k += 64) {
+      const double v = (double)x[k];
+      ss = fma(v, v, ss);
+    }
   }
   ss = wave_sum(ss);
   const double nrm = sqrt(ss);
   // eps == 0: LINAS l2norm (X / norm, NaN on a zero row); eps > 0: F.normalize
   const double inv = (flags & CMVE_PACK_RAW) ? 1.0 : (eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm);
-  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
-  for (int64_t k = lane; k < d_pad; k += 64) {
-    if (k < d) {
-      const double xh = (double)x[k] * inv;
-      if (frow) {
-        const _Float16 hf16 = (_Float16)xh;  // RNE from fp64
-        const double r3 = xh - (double)hf16;
-        e3 = fma(r3, r3, e3);
-        frow[k] = __builtin_bit_cast(uint16_t, hf16);
+  const bool want_f16 = frow != nullptr;
+  PackAcc acc;
+  if constexpr (VEC) {
+    for (int64_t k = lane * 4; k < d_pad; k += 256) {
+      u16x4 hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0}, fv = {0, 0, 0, 0};
+      if (k < d) {  // d % 4 == 0: all four valid
+        const float4 v = *(const float4*)(x + k);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint16_t h, l, f = 0;
+          pack_elem((double)e[c] * inv, want_f16, h, l, f, acc);
+          hv[c] = h;
+          lv[c] = l;
+          fv[c] = f;
+        }
       }
-      const float xf = (float)xh;
-      const uint16_t h = f2bf(xf);
-      const float hf = bf2f(h);
-      const uint16_t l = f2bf(xf - hf);
-      const double r1 = xh - (double)hf;
-      const double r2 = r1 - (double)bf2f(l);
-      e1 = fma(r1, r1, e1);
-      e2 = fma(r2, r2, e2);
+      *(u16x4*)(hrow + k) = hv;
+      if (lrow) *(u16x4*)(lrow + k) = lv;
+      if (frow) *(u16x4*)(frow + k) = fv;
+    }
+  } else {
+    for (int64_t k = lane; k < d_pad; k += 64) {
+      uint16_t h = 0, l = 0, f = 0;
+      if (k < d) pack_elem((double)x[k] * inv, want_f16, h, l, f, acc);
       hrow[k] = h;
       if (lrow) lrow[k] = l;
-    } else {
-      hrow[k] = 0;
-      if (lrow) lrow[k] = 0;
-      if (frow) frow[k] = 0;
+      if (frow) frow[k] = f;
     }
   }
-  e1 = wave_sum(e1);
-  e2 = wave_sum(e2);
-  e3 = wave_sum(e3);
+  const double e1 = wave_sum(acc.e1), e2 = wave_sum(acc.e2), e3 = wave_sum(acc.e3);
   if (lane == 0) {
     inv_norm[row] = inv;
     // sqrt rounding + the fp64 error of x*inv itself (~1e-16 per element) -> small slack
@@ -107,13 +148,36 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
     const float b2 = f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12);
     err_hi[row] = b1;
     err_hilo[row] = b2;
-    if (b1 == b1) atomicMax((int*)&err_max[0], __float_as_int(b1));  // non-negative floats order as ints
-    if (b2 == b2) atomicMax((int*)&err_max[1], __float_as_int(b2));
-    if (err_h16) {
-      const float b3 = f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12);
-      err_h16[row] = b3;
-      if (b3 == b3) atomicMax((int*)&err_max[2], __float_as_int(b3));
-    }
+    if (err_h16) err_h16[row] = f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12);
+  }
+}
+
+// err_max[s] = max over rows of the per-row bounds (NaN rows -- zero rows at eps == 0 -- skipped).
+// One block: a same-address atomic per row serialises at one L2 channel (~30 ns each).
+__global__ __launch_bounds__(1024) void err_max_kernel(const float* __restrict__ e0, const float* __restrict__ e1,
+                                                       const float* __restrict__ e2, int64_t n,
+                                                       float* __restrict__ err_max) {
+  __shared__ float part[3][16];
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f;  // bounds are >= 0
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    m0 = fmaxf(m0, e0[i]);  // fmaxf drops a NaN operand
+    m1 = fmaxf(m1, e1[i]);
+    if (e2) m2 = fmaxf(m2, e2[i]);
+  }
+  m0 = wave_max(m0);
+  m1 = wave_max(m1);
+  m2 = wave_max(m2);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    part[0][w] = m0;
+    part[1][w] = m1;
+    part[2][w] = m2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float m = 0.f;
+    for (int k = 0; k < 16; ++k) m = fmaxf(m, part[threadIdx.x][k]);
+    err_max[threadIdx.x] = m;
   }
 }
 
@@ -166,6 +230,13 @@ int cmve_set_stream(cmve_handle_t h, void* hip_stream) {
 }
 
 int cmve_destroy(cmve_handle_t h) {
+  if (h) {
+    for (hipEvent_t e : h->ev)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h->tev)
+      if (e) (void)hipEventDestroy(e);
+    if (h->aux) (void)hipStreamDestroy(h->aux);
+  }
   delete h;
   return CMVE_OK;
 }
@@ -190,21 +261,29 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
   CMVE_REQUIRE(r->raw_ld >= r->d, "cmve_pack_rows: raw_ld < d");
   CMVE_REQUIRE(r->eps >= 0.0, "cmve_pack_rows: eps < 0");
   CMVE_REQUIRE((r->h16 == nullptr) == (r->err_h16 == nullptr), "cmve_pack_rows: h16 and err_h16 go together");
-  CMVE_HIP(hipMemsetAsync(r->err_max, 0, 3 * sizeof(float), h->stream));
   dim3 grid((unsigned)((r->n_pad + 3) / 4)), block(256);
-  if (r->raw_dtype == CMVE_F32)
-    hipLaunchKernelGGL(pack_rows_kernel<float>, grid, block, 0, h->stream, (const float*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
-                       r->err_h16, r->err_max);
+  const bool vec = r->raw_dtype == CMVE_F32 && r->d % 4 == 0 && r->raw_ld % 4 == 0 &&
+                   (r->n == 0 || ((uintptr_t)r->raw & 15) == 0);
+#define PACK(T, V)                                                                                                   \
+  hipLaunchKernelGGL((pack_rows_kernel<T, V>), grid, block, 0, h->stream, (const T*)r->raw, r->raw_ld, r->n, r->d, \
+                     r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,  \
+                     r->err_h16, r->err_max)
+  if (r->raw_dtype == CMVE_F32 && vec)
+    PACK(float, true);
+  else if (r->raw_dtype == CMVE_F32)
+    PACK(float, false);
   else if (r->raw_dtype == CMVE_F64)
-    hipLaunchKernelGGL(pack_rows_kernel<double>, grid, block, 0, h->stream, (const double*)r->raw, r->raw_ld, r->n,
-                       r->d, r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,
-                       r->err_h16, r->err_max);
+    PACK(double, false);
   else {
     set_error("cmve_pack_rows: raw_dtype must be CMVE_F32 or CMVE_F64");
     return CMVE_E_INVALID;
   }
-  return check_launch("pack_rows");
+#undef PACK
+  int st = check_launch("pack_rows");
+  if (st) return st;
+  hipLaunchKernelGGL(err_max_kernel, dim3(1), dim3(1024), 0, h->stream, r->err_hi, r->err_hilo, r->err_h16, r->n,
+                     r->err_max);
+  return check_launch("pack_rows/err_max");
 }
 
 int cmve_l2norm_rows(cmve_handle_t h, const void* x, int32_t x_dtype, int64_t ldx, void* y, int32_t y_dtype,

@@ -4,11 +4,18 @@
 #include <stdint.h>
 #include <math.h>
 #include <string>
+#include <algorithm>
+#include <type_traits>
 #include "../../include/cmve.h"
 
 struct cmve_handle {
   int device;
   hipStream_t stream;
+  // auxiliary stream + events for cmve_rank_count_overlap (created on first use)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev[CMVE_MAX_CHUNKS + 2] = {};
+  hipEvent_t tev[2 * CMVE_MAX_CHUNKS] = {};  // timing: around each chunk's MFMA pass
+  int last_chunks = 0;
 };
 
 namespace cmve {
@@ -66,10 +73,39 @@ template <typename T> __device__ __forceinline__ double ld64(const T* p) { retur
 // Exact-ish fp64 dot of two raw rows: lane-strided fma chains then a butterfly.
 // The SAME routine serves the GT scores and the fix-up, so a pair scored in both
 // places gets bit-identical values.
+//
+// fp32 x fp32 rows with d % 4 == 0 and 16-B aligned starts (the bench / evaluation layout): lane
+// L owns elements 4L + 256m + c, c = 0..3, accumulated in (m, c) order from float4 loads, four
+// 256-element strides per trip so eight 16-B loads are in flight (the fix-up re-scores ~1e6
+// random pairs: latency, not arithmetic, bounds it).  The order is a function of the pair alone
+// and symmetric in (a, b), so every caller still gets the same bits for the same pair.
 template <typename TA, typename TB>
 __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB* __restrict__ b,
                                              int64_t d, int lane) {
   double acc = 0.0;
+  if constexpr (std::is_same<TA, float>::value && std::is_same<TB, float>::value) {
+    if ((d & 3) == 0 && ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0) {
+      auto fma4 = [&](const float4& x, const float4& y) {
+        acc = fma((double)x.x, (double)y.x, acc);
+        acc = fma((double)x.y, (double)y.y, acc);
+        acc = fma((double)x.z, (double)y.z, acc);
+        acc = fma((double)x.w, (double)y.w, acc);
+      };
+      int64_t k = (int64_t)lane * 4;
+      for (; k + 768 < d; k += 1024) {
+        const float4 a0 = *(const float4*)(a + k), a1 = *(const float4*)(a + k + 256);
+        const float4 a2 = *(const float4*)(a + k + 512), a3 = *(const float4*)(a + k + 768);
+        const float4 b0 = *(const float4*)(b + k), b1 = *(const float4*)(b + k + 256);
+        const float4 b2 = *(const float4*)(b + k + 512), b3 = *(const float4*)(b + k + 768);
+        fma4(a0, b0);
+        fma4(a1, b1);
+        fma4(a2, b2);
+        fma4(a3, b3);
+      }
+      for (; k < d; k += 256) fma4(*(const float4*)(a + k), *(const float4*)(b + k));
+      return wave_sum(acc);
+    }
+  }
   for (int64_t k = lane; k < d; k += WAVE) acc = fma(ld64(a + k), ld64(b + k), acc);
   return wave_sum(acc);
 }

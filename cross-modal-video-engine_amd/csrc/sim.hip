@@ -39,6 +39,7 @@ struct SimArgs {
   int nq, ng;
   int nblk_m, nblk_n;
   int nk;
+  int gn;  // gallery tiles per tile-order group
   // linear epilogue: v = acc + bias; act; + resid; v * bn_scale + bn_shift
   const float* bias;
   const float* bn_scale;
@@ -64,12 +65,11 @@ struct SimArgs {
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
-__device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, int& bm, int& bn) {
+__device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, int GN, int& bm, int& bn) {
   const int total = nblk_m * nblk_n;
   const int xcd = bid & 7, local = bid >> 3;
   const int q = total >> 3, r = total & 7;
   const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-  constexpr int GN = 8;
   const int group = L / (GN * nblk_m);
   const int within = L - group * (GN * nblk_m);
   const int gn = min(GN, nblk_n - group * GN);
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
   const int wr = wave / WN, wc = wave % WN;
   int bm, bn;
-  tile_of_block(blockIdx.x, a.nblk_m, a.nblk_n, bm, bn);
+  tile_of_block(blockIdx.x, a.nblk_m, a.nblk_n, a.gn, bm, bn);
   const int m0 = bm * BM, n0 = bn * BN;
 
   // epilogue scratch after the staging buffers (one dynamic LDS object only)
@@ -517,6 +517,11 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
   }
   a.nblk_m = (int)(nq_pad / G::BM);
   a.nblk_n = (int)(ng_pad / G::BN);
+  static const int gn_env = [] {
+    const char* e = getenv("CMVE_SIM_GN");  // kernel studies only
+    return e ? atoi(e) : 0;
+  }();
+  a.gn = gn_env > 0 ? gn_env : 8;
   const unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
   hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, PHASED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
   return check_launch("sim_kernel");
@@ -668,6 +673,115 @@ extern "C" int cmve_rank_count(cmve_handle_t h, const cmve_rows_t* q, const cmve
                           cand_count);
   if (st) return st;
   return cmve_rank_fixup(h, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, cand_count);
+}
+
+static size_t elem_bytes(int32_t dt) { return (dt == CMVE_F64 || dt == CMVE_I64) ? 8 : dt == CMVE_BF16 ? 2 : 4; }
+
+// rows [r0, r0 + rows_pad) of a packed set as a packed set of its own (err_max stays the whole
+// set's: a valid, slightly looser bound for the chunk)
+static cmve_rows_t chunk_view(const cmve_rows_t* g, int64_t r0, int64_t rows_pad) {
+  cmve_rows_t v = *g;
+  v.n = std::max<int64_t>(0, std::min<int64_t>(g->n - r0, rows_pad));
+  v.n_pad = rows_pad;
+  const int64_t e = r0 * g->d_pad;
+  if (g->hi) v.hi = g->hi + e;
+  if (g->lo) v.lo = g->lo + e;
+  if (g->h16) v.h16 = g->h16 + e;
+  if (g->raw) v.raw = (const char*)g->raw + r0 * g->raw_ld * (int64_t)elem_bytes(g->raw_dtype);
+  if (g->inv_norm) v.inv_norm = g->inv_norm + r0;
+  if (g->err_hi) v.err_hi = g->err_hi + r0;
+  if (g->err_hilo) v.err_hilo = g->err_hilo + r0;
+  if (g->err_h16) v.err_h16 = g->err_h16 + r0;
+  return v;
+}
+
+static int ensure_aux(cmve_handle_t h) {
+  if (h->aux) return CMVE_OK;
+  int cur = 0;
+  CMVE_HIP(hipGetDevice(&cur));
+  CMVE_HIP(hipSetDevice(h->device));
+  hipError_t e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
+  for (int i = 0; e == hipSuccess && i < CMVE_MAX_CHUNKS + 2; ++i)
+    e = hipEventCreateWithFlags(&h->ev[i], hipEventDisableTiming);
+  for (int i = 0; e == hipSuccess && i < 2 * CMVE_MAX_CHUNKS; ++i) e = hipEventCreate(&h->tev[i]);
+  (void)hipSetDevice(cur);
+  CMVE_HIP(e);
+  return CMVE_OK;
+}
+
+extern "C" int cmve_rank_count_overlap(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode,
+                                       int32_t dirs, const double* row_sgt, const float* row_hi, const float* row_lo,
+                                       const double* col_sgt, const float* col_hi, const float* col_lo,
+                                       int32_t* row_cnt, int32_t* col_cnt, uint64_t* cand, int64_t cand_cap,
+                                       int64_t* cand_count, int32_t chunks) {
+  CMVE_REQUIRE(h, "cmve_rank_count_overlap: NULL handle");
+  CMVE_REQUIRE(chunks >= 1 && chunks <= CMVE_MAX_CHUNKS, "cmve_rank_count_overlap: chunks must be in [1, %d]",
+               CMVE_MAX_CHUNKS);
+  if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_sgt, "cmve_rank_count_overlap: row_sgt missing");
+  if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_sgt, "cmve_rank_count_overlap: col_sgt missing");
+  SimArgs a;
+  int st = rank_args(q, g, mode, dirs, row_hi, row_lo, col_hi, col_lo, row_cnt, col_cnt, cand, cand_cap, cand_count,
+                     a, "cmve_rank_count_overlap");
+  if (st) return st;
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_count_overlap: raw rows / norms missing");
+  hipStream_t s0 = h->stream;
+  CMVE_HIP(hipMemsetAsync(cand_count, 0, sizeof(int64_t) * chunks, s0));
+  if (dirs & CMVE_DIR_ROW) CMVE_HIP(hipMemsetAsync(row_cnt, 0, sizeof(int32_t) * q->n_pad, s0));
+  if (dirs & CMVE_DIR_COL) CMVE_HIP(hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * g->n_pad, s0));
+  if (q->n == 0 || g->n == 0) return CMVE_OK;
+  st = ensure_aux(h);
+  if (st) return st;
+  // chunk rows: a multiple of CMVE_ROW_ALIGN covering g->n_pad in `chunks` pieces
+  const int64_t units = g->n_pad / CMVE_ROW_ALIGN;
+  const int64_t per = ((units + chunks - 1) / chunks) * CMVE_ROW_ALIGN;
+  const int64_t cap_c = cand_cap / chunks;
+  CMVE_HIP(hipEventRecord(h->ev[0], s0));
+  CMVE_HIP(hipStreamWaitEvent(h->aux, h->ev[0], 0));
+  int used = 0;
+  for (int c = 0; c < chunks; ++c) {
+    const int64_t r0 = (int64_t)c * per;
+    if (r0 >= g->n) break;
+    const cmve_rows_t v = chunk_view(g, r0, std::min<int64_t>(per, g->n_pad - r0));
+    SimArgs ac = a;
+    ac.ghi = mode == CMVE_SIM_F16 ? v.h16 : v.hi;
+    ac.glo = v.lo;
+    ac.ng = (int)v.n;
+    if (dirs & CMVE_DIR_COL) {
+      ac.col_hi = col_hi + r0;
+      ac.col_lo = col_lo + r0;
+      ac.col_cnt = col_cnt + r0;
+    }
+    ac.cand = (unsigned long long*)(cand + c * cap_c);
+    ac.cand_cap = cap_c;
+    ac.cand_count = (unsigned long long*)(cand_count + c);
+    CMVE_HIP(hipEventRecord(h->tev[2 * c], s0));
+    st = dispatch<EPI_RANK>(ac, q, &v, mode, s0);
+    if (st) return st;
+    CMVE_HIP(hipEventRecord(h->tev[2 * c + 1], s0));
+    CMVE_HIP(hipEventRecord(h->ev[1 + c], s0));
+    CMVE_HIP(hipStreamWaitEvent(h->aux, h->ev[1 + c], 0));
+    st = launch_fixup(h->aux, q, &v, dirs, row_sgt, (dirs & CMVE_DIR_COL) ? col_sgt + r0 : nullptr, row_cnt,
+                      (dirs & CMVE_DIR_COL) ? col_cnt + r0 : nullptr, cand + c * cap_c, cap_c, cand_count + c);
+    if (st) return st;
+    used = c + 1;
+  }
+  h->last_chunks = used;
+  CMVE_HIP(hipEventRecord(h->ev[CMVE_MAX_CHUNKS + 1], h->aux));
+  CMVE_HIP(hipStreamWaitEvent(s0, h->ev[CMVE_MAX_CHUNKS + 1], 0));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_overlap_mfma_ms(cmve_handle_t h, float* ms, int32_t* launches) {
+  CMVE_REQUIRE(h && ms && launches, "cmve_overlap_mfma_ms: NULL argument");
+  *ms = 0.f;
+  *launches = h->last_chunks;
+  for (int c = 0; c < h->last_chunks; ++c) {
+    float t = 0.f;
+    CMVE_HIP(hipEventSynchronize(h->tev[2 * c + 1]));
+    CMVE_HIP(hipEventElapsedTime(&t, h->tev[2 * c], h->tev[2 * c + 1]));
+    *ms += t;
+  }
+  return CMVE_OK;
 }
 
 extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_rows_t* w, int32_t mode, const float* bias,

@@ -254,6 +254,29 @@ int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g,
                     const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count);
 
 /*
+ * cmve_rank_count with the fix-up hidden behind the MFMA pass: the gallery `g` is cut into
+ * `chunks` row ranges (multiples of CMVE_ROW_ALIGN); chunk c's MFMA pass runs on the handle's
+ * stream and its fp64 fix-up on an auxiliary stream of the handle as soon as that pass is done,
+ * overlapping chunk c+1's MFMA pass.  Chunk c appends to cand[c*cap_c, (c+1)*cap_c) with
+ * cap_c = cand_cap / chunks and counts into cand_count[c] (device int64[chunks]); if any
+ * cand_count[c] > cap_c the counts are incomplete: retry with a larger cand_cap.  Results are
+ * identical to cmve_rank_count.  Returns with all work ordered before later work on the handle's
+ * stream.  1 <= chunks <= CMVE_MAX_CHUNKS.
+ * Replaces: the single-stream argsort loop of LINAS-engine/util/metrics.py:137-147 (as cmve_rank_count).
+ */
+#define CMVE_MAX_CHUNKS 16
+int cmve_rank_count_overlap(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode,
+                            int32_t dirs,
+                            const double* row_sgt, const float* row_hi, const float* row_lo,
+                            const double* col_sgt, const float* col_hi, const float* col_lo,
+                            int32_t* row_cnt, int32_t* col_cnt,
+                            uint64_t* cand, int64_t cand_cap, int64_t* cand_count, int32_t chunks);
+/* Summed duration of the MFMA passes of the handle's last cmve_rank_count_overlap (timing events
+ * recorded on the handle's stream around each chunk's pass; waits for the last one) and the
+ * number of passes: the per-launch duration a roofline figure needs while the fix-ups overlap. */
+int cmve_overlap_mfma_ms(cmve_handle_t h, float* ms, int32_t* launches);
+
+/*
  * Thresholds from GIVEN exact GT scores sgt[a_set->n] (NaN = no GT): the sharded path,
  * where the owner rank of a query's GT computes sgt and all-gathers it with the query.
  * thr_hi/thr_lo as cmve_gt_thresholds, against the error bound of `b_set` (the local shard).

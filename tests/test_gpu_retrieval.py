@@ -248,3 +248,56 @@ def test_full_size_c3_against_independent_fp64(torch_cuda):
     exp_c += 1
     # ties / near-ties at 1e-13 could legitimately differ between two fp64 summation orders
     assert (t2v != exp_r).sum() <= 2 and (v2t != exp_c).sum() <= 2
+
+
+@pytest.mark.parametrize("nq,ng,d,chunks", [(300, 5000, 256, 3), (64, 300, 100, 7), (257, 2049, 640, 2),
+                                            (5, 1, 64, 4), (1000, 1000, 1024, 16)])
+def test_overlap_chunks_match_oracle(torch_cuda, nq, ng, d, chunks):
+    """cmve_rank_count_overlap (gallery chunks, fix-ups on the auxiliary stream) == the oracle's
+    exact fp64 counts, both directions, including chunk counts past the gallery's end."""
+    from cmve import engine
+    rng = np.random.default_rng(nq + 31 * ng + chunks)
+    gal = rng.standard_normal((ng, d))
+    qs = gal[rng.integers(0, ng, nq)] + 3.0 * rng.standard_normal((nq, d))
+    row_gts = [[] if i % 11 == 10 else [int(rng.integers(0, ng))] for i in range(nq)]
+    col_gts = [[int(x) for x in rng.choice(nq, size=min(nq, 1 + j % 3), replace=False)] for j in range(ng)]
+    s = R.exact_scores64(qs, gal)
+    q = engine.RowSet(qs, with_lo=False)
+    g = engine.RowSet(gal, with_lo=False)
+    r, c, _ = engine.gt_rank_counts(q, g, row_gts=row_gts, col_gts=col_gts, chunks=chunks)
+    assert np.array_equal(r, R.rank_counts(s, row_gts))
+    assert np.array_equal(c, R.rank_counts(s.T, col_gts))
+
+
+def test_overlap_overflow_retry(torch_cuda):
+    from cmve import engine
+    v, c, vid, cid = _c1()
+    v2t_gt, t2v_gt = R.get_gt(vid, cid)
+    caps = engine.RowSet(c, with_lo=False)
+    vids = engine.RowSet(v, with_lo=False)
+    ws = engine.RankWorkspace(caps.device, cap=16)  # 4 per chunk: forces the grow-and-retry path
+    rows = [t2v_gt[i] for i in range(1000)]
+    t2v, v2t, ncand = engine.gt_rank_counts(caps, vids, row_gts=rows, col_gts=v2t_gt, ws=ws, chunks=4)
+    assert ncand > 16
+    s = -R.cal_error(v, c)
+    assert np.array_equal(t2v, R.rank_counts(s, rows))
+    assert np.array_equal(v2t, R.rank_counts(s.T, v2t_gt))
+
+
+def test_overlap_full_size_equals_single_pass(torch_cuda):
+    """Bench-shaped shard slice (16,384 x 32,768 x 1024): chunked + overlapped counts are
+    bit-identical to the single-pass counts (same exact fp64 re-score of the same pairs)."""
+    from cmve import engine
+    torch = torch_cuda
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    ng, nq, d = 32768, 16384, 1024
+    g = torch.randn((ng, d), generator=gen, device="cuda")
+    gt = torch.randint(0, ng, (nq,), generator=gen, device="cuda")
+    q = (g[gt] + 10.0 * torch.randn((nq, d), generator=gen, device="cuda")).contiguous()
+    G = engine.RowSet(g, with_lo=False)
+    Q = engine.RowSet(q, with_lo=False)
+    rows = [[int(x)] for x in gt.cpu().numpy()]
+    r1, _, n1 = engine.gt_rank_counts(Q, G, row_gts=rows, chunks=1)
+    r4, _, n4 = engine.gt_rank_counts(Q, G, row_gts=rows, chunks=4)
+    assert n1 > 0 and n1 == n4
+    assert np.array_equal(r1, r4)

@@ -37,6 +37,8 @@ def main():
     q = (g[gt] + 10.0 * torch.randn((nq, d), generator=gen, device=dev)).contiguous()
     G = engine.RowSet(g, with_lo=True, with_f16=True)
     Q = engine.RowSet(q, with_lo=True, with_f16=True)
+    t_pack = timed(lambda: engine.RowSet(q, with_lo=False, with_f16=True))
+    print(json.dumps({"pack_queries_ms": t_pack, "rows": nq, "dim": d}), flush=True)
     off, idx = engine.csr([[int(x)] for x in gt.cpu().numpy()], dev)
     ws = engine.RankWorkspace(dev, cap=1 << 25)
     inf = torch.full((Q.n_pad,), float("inf"), dtype=torch.float32, device=dev)
@@ -60,15 +62,18 @@ def main():
                                                 ws.cap, engine._ptr(ws.count)))
         t_plain = timed(lambda: mfma(inf, inf))
         t_rank = timed(lambda: mfma(hi, lo))
-        ncand = int(ws.count.item())
+        ncand = int(ws.count[0].item())
         t_fix = timed(fix) if not os.environ.get("KB_NOFIX") else float("nan")  # diagnostic builds: garbage pairs
         E = float((hi - lo)[:nq].double().mean().item()) / 2
         mult = 3 if mode == _lib.SIM_BF16X3 else 1
         print(json.dumps({"mode": name, "gemm_only_ms": t_plain, "rank_mfma_ms": t_rank, "fixup_ms": t_fix,
                           "candidates": ncand, "mean_E": E, "tflops_gemm_only": flops * mult / t_plain / 1e9,
                           "tflops_rank": flops * mult / t_rank / 1e9}), flush=True)
-    t_store = timed(lambda: engine.sim_store(Q, G, mode=_lib.SIM_BF16) if False else None)
-    del t_store
+        if name == "F16":  # whole rank count (MFMA + fix-up), fix-ups overlapped across gallery chunks
+            for ch in (1, 2, 4, 8):
+                t = timed(lambda: engine.rank_count_launch(Q, G, mode, row=(sgt, hi, lo), ws=ws, chunks=ch))
+                print(json.dumps({"mode": name, "chunks": ch, "rank_count_ms": t, "candidates": ws.ncand()}),
+                      flush=True)
 
 
 if __name__ == "__main__":

@@ -34,7 +34,7 @@ def main(outdir, tag):
         vals = []
         for r in rows(os.path.join(outdir, sub, "**", "*counter_collection.csv")):
             name = r.get("Kernel_Name", "")
-            if "sim_kernel" in name and ("<2, 1>" in name or "ILi2ELi1E" in name) and r.get("Counter_Name") == counter:
+            if "sim_kernel" in name and ("<2, 1" in name or "ILi2ELi1E" in name) and r.get("Counter_Name") == counter:
                 vals.append(float(r["Counter_Value"]))
         res[counter] = vals
     f = res["FETCH_SIZE"]
@@ -44,7 +44,7 @@ def main(outdir, tag):
            "write_kib_per_launch": (sum(w) / len(w)) if w else None}
     if f and w:
         out["hbm_bytes_per_launch"] = 2 * out["fetch_kib_per_launch"] * 1024 + out["write_kib_per_launch"] * 1024
-    out.update({"shard": 131072, "nq": 16384, "dim": 1024,
+    out.update({"shard": 131072, "nq": 16384, "dim": 1024, "chunks": 1,
                 "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"})
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
     print(json.dumps(out))
