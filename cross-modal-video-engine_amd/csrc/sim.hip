@@ -99,6 +99,51 @@ __device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chu
   return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
 
+// sum over the 16 lanes of each DPP row (quad xor 1, xor 2, half-row mirror, row mirror): 4 VALU
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return v;
+}
+
+// One row's 4 scores against its thresholds, hand-scheduled: count = #{s > hi} (exact v_cmp,
+// NaN never counts) and a lane mask of "some s in [lo, hi]" (v_med3 clamp == s).  The compiler
+// routes every compare through VCC and pads each with s_nop 1 before the reader; here the four
+// masks go to separate SGPR pairs and are read >= 3 instructions later (no wait states needed).
+__device__ __forceinline__ uint32_t row4_count_hit(float s0, float s1, float s2, float s3, float hi, float lo,
+                                                   unsigned long long& hit) {
+  uint32_t c;
+  float t0, t1, t2, t3;
+  unsigned long long m0, m1, m2, m3, h, cc;
+  asm("v_cmp_gt_f32_e64 %[m0], %[s0], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m1], %[s1], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m2], %[s2], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m3], %[s3], %[hi]\n\t"
+      "v_med3_f32 %[t0], %[s0], %[lo], %[hi]\n\t"
+      "v_med3_f32 %[t1], %[s1], %[lo], %[hi]\n\t"
+      "v_med3_f32 %[t2], %[s2], %[lo], %[hi]\n\t"
+      "v_med3_f32 %[t3], %[s3], %[lo], %[hi]\n\t"
+      "v_cndmask_b32_e64 %[c], 0, 1, %[m0]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m1]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m2]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m3]\n\t"
+      "v_cmp_eq_f32_e64 %[m0], %[t0], %[s0]\n\t"
+      "v_cmp_eq_f32_e64 %[m1], %[t1], %[s1]\n\t"
+      "v_cmp_eq_f32_e64 %[m2], %[t2], %[s2]\n\t"
+      "v_cmp_eq_f32_e64 %[m3], %[t3], %[s3]\n\t"
+      "s_nop 1\n\t"
+      "s_or_b64 %[h], %[m0], %[m1]\n\t"
+      "s_or_b64 %[h], %[h], %[m2]\n\t"
+      "s_or_b64 %[h], %[h], %[m3]"
+      : [c] "=&v"(c), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [m0] "=&s"(m0),
+        [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [h] "=&s"(h), [cc] "=&s"(cc)
+      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [hi] "v"(hi), [lo] "v"(lo));
+  hit |= h;
+  return c;
+}
+
 template <int MODE>
 __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
   if constexpr (MODE == CMVE_SIM_F16)
@@ -123,8 +168,21 @@ constexpr size_t stage_bytes() {
   return (size_t)((MODE == CMVE_SIM_BF16X3) ? 2 : 1) * (BM + BN) * BK * 2;
 }
 
+#ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
+#define CMVE_STAMP(k) \
+  if (threadIdx.x == 0) a.cand[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define CMVE_STAMP(k)
+#endif
+
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
+  CMVE_STAMP(0);
+#ifdef CMVE_DBG_STAMPS  // where the block ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4)
+  if (threadIdx.x == 0)
+    a.cand[(size_t)blockIdx.x * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                          (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -145,9 +203,24 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   unsigned long long* lds_cand = (unsigned long long*)(lds_cc + BN);
   unsigned* lds_ncand = (unsigned*)(lds_cand + CAND_LDS);
   unsigned long long* lds_cand_base = (unsigned long long*)(lds_ncand + 2);
-  if (EPI == EPI_RANK) {
+  // rank thresholds of the tile: [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
+  float* lds_thr = (float*)(lds_cand_base + 1);
+  float thr_hi_v = __builtin_nanf(""), thr_lo_v = __builtin_nanf("");
+  if constexpr (EPI == EPI_RANK) {
+    static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
     if (tid == 0) *lds_ncand = 0u;
+    // fetched now, published to LDS after the main loop: the epilogue must not wait on HBM
+    // (8 dependent threshold loads per wave inside it cost ~28% of the kernel)
+    if (tid < BM) {
+      if (a.row_hi) {
+        thr_hi_v = a.row_hi[m0 + tid];
+        thr_lo_v = a.row_lo[m0 + tid];
+      }
+    } else if (a.col_hi) {
+      thr_hi_v = a.col_hi[n0 + tid - BM];
+      thr_lo_v = a.col_lo[n0 + tid - BM];
+    }
   }
 
   auto stage = [&](int t, int s) {
@@ -260,6 +333,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     CMVE_BAR();
+    CMVE_STAMP(1);
     if (wr == 1) { CMVE_BAR(); }  // stagger: group 1 runs one barrier behind
     for (int t = 0; t < nk; ++t) {
       const char* buf = smem + (t & 1) * STAGE_BYTES;
@@ -292,6 +366,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       CMVE_BAR();
     }
     if (wr == 0) { CMVE_BAR(); }  // re-align the barrier counts of the two groups
+    CMVE_STAMP(2);
 #undef CMVE_BAR
   } else {
   stage(0, 0);
@@ -361,6 +436,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   }
   }
 
+#ifdef CMVE_DBG_NOEPI  // diagnostic build only: main loop without any epilogue (results are garbage)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+  return;
+#endif
   // ---------------- epilogues ----------------
   // accumulator element (i, j, r): row = m0 + wr*TM*16 + i*16 + (lane>>4)*4 + r,
   //                                col = n0 + wc*TN*16 + j*16 + (lane&15)
@@ -415,57 +497,56 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         }
       }
   } else {
-    // thresholds; a disabled direction gets NaN, which no comparison passes (not even s = +inf)
+    // thresholds from LDS; a disabled direction holds NaN, which no comparison passes (not even s = +inf)
+    lds_thr[tid] = thr_hi_v;
+    lds_thr[NT + tid] = thr_lo_v;
+    __syncthreads();
+    CMVE_STAMP(4);
+    const float* l_rhi = lds_thr + (rbase - m0);
+    const float* l_rlo = lds_thr + NT + (rbase - m0);
     float chi[TN], clo[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      chi[j] = a.col_hi ? a.col_hi[cbase + j * 16] : __builtin_nanf("");
-      clo[j] = a.col_lo ? a.col_lo[cbase + j * 16] : __builtin_nanf("");
+      chi[j] = lds_thr[BM + (cbase - n0) + j * 16];
+      clo[j] = lds_thr[NT + BM + (cbase - n0) + j * 16];
     }
+    // Branch-free scoring pass: per score only compares and bit packing.  Undecided pairs are
+    // recorded as bits (per i: bit j*4+r = row-undecided, bit 16+j*4+r = column-undecided) and
+    // emitted afterwards with ONE LDS atomic per wave; a per-score atomic with exec-mask
+    // branches cost ~40% of the block (s_memtime stamps, tools/kbench.py KB_STAMPS).
     const bool padded = (m0 + BM > a.nq) || (n0 + BN > a.ng);
-    uint32_t cc_pack = 0u;  // byte j: count for column j (<= 4*TM per lane, <= 16*TM after the reduce)
+    uint32_t rowok = 0xffffffffu, colok = 0xfu;  // bit i*4+r / bit j: inside the real n_q x n_g
+    if (padded) {
+      rowok = 0u;
+      colok = 0u;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      f32x4_t rhi, rlo;
-      if (a.row_hi) {
-        rhi = *(const f32x4_t*)(a.row_hi + rbase + i * 16);
-        rlo = *(const f32x4_t*)(a.row_lo + rbase + i * 16);
-      } else {
-        const float qnan = __builtin_nanf("");
-        rhi = f32x4_t{qnan, qnan, qnan, qnan};
-        rlo = rhi;
-      }
-      uint32_t rc_pack = 0u;  // byte r: count for row (i, r) over this lane's TN columns
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rowok |= (uint32_t)(rbase + i * 16 + r < a.nq) << (i * 4 + r);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) colok |= (uint32_t)(cbase + j * 16 < a.ng) << j;
+    }
+    uint32_t cc_pack = 0u;  // byte j: count for column j (<= 4*TM per lane, <= 16*TM after the reduce)
+    uint32_t und[TM];
+    // exact undecided bits of one i-block: lo <= s <= hi from its own compares (reusing
+    // "!(s > hi)" kept 128 lane masks live and spilled them); a disabled direction is skipped
+    auto und_bits = [&](int i, const f32x4_t& rhi, const f32x4_t& rlo, bool dr, bool dc, auto padded_c) {
+      constexpr bool PAD = decltype(padded_c)::value;
+      uint32_t u = 0u;
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float s = acc[i][j][r];
-          const int row = rbase + i * 16 + r;
-          const int col = cbase + j * 16;
-          if (padded && (row >= a.nq || col >= a.ng)) s = -INFINITY;
-          const bool br = s > rhi[r];
-          const bool bc = s > chi[j];
-          rc_pack += (uint32_t)br << (8 * r);
-          cc_pack += (uint32_t)bc << (8 * j);
-          const uint32_t flags = (uint32_t)((s >= rlo[r]) & !br) | ((uint32_t)((s >= clo[j]) & !bc) << 1);
-          if (flags) {
-            const unsigned long long packed =
-                (unsigned long long)row | ((unsigned long long)col << 31) | ((unsigned long long)flags << 62);
-            const unsigned p = atomicAdd(lds_ncand, 1u);
-            if (p < (unsigned)CAND_LDS) {
-              lds_cand[p] = packed;
-            } else {  // block buffer full: straight to the global list
-              const unsigned long long slot = atomicAdd(a.cand_count, 1ull);
-              if ((long long)slot < a.cand_cap) a.cand[slot] = packed;
-            }
-          }
+          float sc = acc[i][j][r];
+          if constexpr (PAD) sc = ((rowok >> (i * 4 + r)) & (colok >> j) & 1u) ? sc : -INFINITY;
+          if (dr) u |= ((sc >= rlo[r] && sc <= rhi[r]) ? 1u : 0u) << (j * 4 + r);
+          if (dc) u |= ((sc >= clo[j] && sc <= chi[j]) ? 1u : 0u) << (16 + j * 4 + r);
         }
-      // rows: reduce over the 16 lanes that share (lane >> 4); bytes stay <= 64
-      rc_pack += __shfl_xor(rc_pack, 1, 64);
-      rc_pack += __shfl_xor(rc_pack, 2, 64);
-      rc_pack += __shfl_xor(rc_pack, 4, 64);
-      rc_pack += __shfl_xor(rc_pack, 8, 64);
+      return u;
+    };
+    auto row_reduce = [&](int i, uint32_t rc_pack) {
+      // rows: sum over the 16 lanes of a DPP row (those sharing lane >> 4); bytes stay <= 64
+      rc_pack = row_sum16(rc_pack);
       if ((lane & 15) == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -473,6 +554,85 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           if (c) atomicAdd(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
         }
       }
+    };
+    const bool do_row = a.row_hi != nullptr, do_col = a.col_hi != nullptr;
+    // fast scoring of an unpadded tile: per score an exact count compare (v_cmp + v_addc) and an
+    // "inside [lo, hi]" test (v_med3 + v_cmp) folded into a wave mask; the exact undecided bits
+    // are recomputed only for i-blocks where some lane hit.  The epilogue is VALU-issue-bound
+    // (4 cycles per wave64 instruction x 128 scores per lane): every instruction per score counts.
+    auto fast_block = [&](auto row_c, auto col_c) {
+      constexpr bool DR = decltype(row_c)::value, DC = decltype(col_c)::value;
+      uint32_t ccnt[TN] = {};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4_t rhi = {}, rlo = {};
+        if constexpr (DR) {
+          rhi = *(const f32x4_t*)(l_rhi + i * 16);
+          rlo = *(const f32x4_t*)(l_rlo + i * 16);
+        }
+        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
+        bool hit = false;
+        if constexpr (DR && !DC && TN == 4) {  // the bench / t2v shape: hand-scheduled per row
+          unsigned long long hm = 0ull;
+          c0 = row4_count_hit(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], hm);
+          c1 = row4_count_hit(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], hm);
+          c2 = row4_count_hit(acc[i][0][2], acc[i][1][2], acc[i][2][2], acc[i][3][2], rhi[2], rlo[2], hm);
+          c3 = row4_count_hit(acc[i][0][3], acc[i][1][3], acc[i][2][3], acc[i][3][3], rhi[3], rlo[3], hm);
+          hit = hm != 0ull;  // wave-uniform
+        } else
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const f32x4_t sc = acc[i][j];
+          if constexpr (DR) {
+            c0 += sc[0] > rhi[0];
+            c1 += sc[1] > rhi[1];
+            c2 += sc[2] > rhi[2];
+            c3 += sc[3] > rhi[3];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hit |= __builtin_amdgcn_fmed3f(sc[r], rlo[r], rhi[r]) == sc[r];
+          }
+          if constexpr (DC) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              ccnt[j] += sc[r] > chi[j];
+              hit |= __builtin_amdgcn_fmed3f(sc[r], clo[j], chi[j]) == sc[r];
+            }
+          }
+        }
+        if constexpr (DR) row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+        und[i] = __builtin_amdgcn_ballot_w64(hit) ? und_bits(i, rhi, rlo, DR, DC, std::false_type{}) : 0u;
+      }
+      if constexpr (DC) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) cc_pack += ccnt[j] << (8 * j);
+      }
+    };
+    if (padded) {  // boundary tiles: generic, masked
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        const f32x4_t rhi = *(const f32x4_t*)(l_rhi + i * 16);
+        const f32x4_t rlo = *(const f32x4_t*)(l_rlo + i * 16);
+        uint32_t rc_pack = 0u;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float sc = acc[i][j][r];
+            sc = ((rowok >> (i * 4 + r)) & (colok >> j) & 1u) ? sc : -INFINITY;
+            rc_pack += (sc > rhi[r] ? 1u : 0u) << (8 * r);
+            cc_pack += (sc > chi[j] ? 1u : 0u) << (8 * j);
+          }
+        und[i] = und_bits(i, rhi, rlo, do_row, do_col, std::true_type{});
+        row_reduce(i, rc_pack);
+      }
+    } else if (do_row && do_col) {
+      fast_block(std::true_type{}, std::true_type{});
+    } else if (do_row) {
+      fast_block(std::true_type{}, std::false_type{});
+    } else {
+      fast_block(std::false_type{}, std::true_type{});
     }
     cc_pack += __shfl_xor(cc_pack, 16, 64);
     cc_pack += __shfl_xor(cc_pack, 32, 64);
@@ -483,6 +643,46 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         if (c) atomicAdd(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
       }
     }
+    CMVE_STAMP(5);
+    // emission: wave-inclusive scan of the per-lane counts, one LDS atomic per wave
+    uint32_t nmine = 0u;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) nmine += __builtin_popcount((und[i] | (und[i] >> 16)) & 0xffffu);
+    // exclusive prefix of nmine over lanes from one ballot per count bit (mbcnt = popcount of
+    // the lower lanes); nmine <= 16*TM < 256.  No LDS round trips (a __shfl scan is 6 bpermutes).
+    uint32_t excl = 0u, total = 0u;
+    if (__builtin_amdgcn_ballot_w64(nmine != 0u)) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const unsigned long long m = __builtin_amdgcn_ballot_w64((nmine >> b) & 1u);
+        excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+        total += (uint32_t)__builtin_popcountll(m) << b;
+      }
+    }
+    if (total) {
+      uint32_t base = 0u;
+      if (lane == 0) base = atomicAdd(lds_ncand, total);
+      base = __builtin_amdgcn_readfirstlane(base) + excl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        uint32_t m = (und[i] | (und[i] >> 16)) & 0xffffu;
+        while (m) {
+          const int bit = __builtin_ctz(m);
+          m &= m - 1u;
+          const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
+          const unsigned long long packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
+                                            ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
+          if (base < (uint32_t)CAND_LDS) {
+            lds_cand[base] = packed;
+          } else {  // block buffer full: straight to the global list
+            const unsigned long long slot = atomicAdd(a.cand_count, 1ull);
+            if ((long long)slot < a.cand_cap) a.cand[slot] = packed;
+          }
+          ++base;
+        }
+      }
+    }
+    CMVE_STAMP(6);
     __syncthreads();
     // flush the block's undecided pairs with ONE global atomic
     const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
@@ -501,6 +701,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
       }
     }
+#ifdef CMVE_DBG_STAMPS
+    __syncthreads();
+#endif
+    CMVE_STAMP(3);
   }
 }
 
@@ -508,7 +712,9 @@ template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
   const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN>() +
-                     (EPI == EPI_RANK ? (G::BM + G::BN) * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 : 0);
+                     (EPI == EPI_RANK ? (G::BM + G::BN) * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 +
+                                            2 * (G::BM + G::BN) * sizeof(float)
+                                      : 0);
   static bool attr_done = false;
   if (!attr_done) {
     CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,

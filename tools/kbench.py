@@ -61,6 +61,42 @@ def main():
                                                 engine._ptr(sgt), None, engine._ptr(cnt), None, engine._ptr(ws.cand),
                                                 ws.cap, engine._ptr(ws.count)))
         t_plain = timed(lambda: mfma(inf, inf))
+        if os.environ.get("KB_STAMPS"):  # libcmve_STAMPS.so: per-block s_memtime stamps in ws.cand
+            mfma(inf, inf)
+            torch.cuda.synchronize()
+            nblk = (Q.n_pad // 256) * (G.n_pad // 256)
+            st = ws.cand[:nblk * 8].view(nblk, 8).cpu().numpy().astype(np.float64)
+            d = np.diff(st[:, :4], axis=1)
+            span = st[:, 3].max() - st[:, 0].min()
+            med = lambda x: float(np.median(x))  # noqa: E731
+            print(json.dumps({"stamps": {"prologue_cyc": med(d[:, 0]), "main_cyc": med(d[:, 1]),
+                                         "epilogue_cyc": med(d[:, 2]),
+                                         "epi_thr_publish": med(st[:, 4] - st[:, 2]),
+                                         "epi_scoring": med(st[:, 5] - st[:, 4]),
+                                         "epi_emission": med(st[:, 6] - st[:, 5]),
+                                         "epi_flush_atomics": med(st[:, 3] - st[:, 6]),
+                                         "block_total_cyc": float(np.median(st[:, 3] - st[:, 0])),
+                                         "kernel_span_cyc": float(span), "blocks": nblk,
+                                         "sum_block_cyc_per_cu": float((st[:, 3] - st[:, 0]).sum() / 256)}}),
+                  flush=True)
+            # per-CU timelines: gap between a block's end and the next block's start on the same CU
+            hw = ws.cand[:nblk * 8].view(nblk, 8)[:, 7].cpu().numpy().astype(np.uint64)
+            hwid = hw & np.uint64(0xffffffff)
+            cu = (hw >> np.uint64(32)) * np.uint64(4096) + ((hwid >> np.uint64(8)) & np.uint64(0xf)) + \
+                np.uint64(16) * ((hwid >> np.uint64(12)) & np.uint64(0x7))  # xcc, cu_id, sh/se bits
+            gaps = []
+            per_cu = {}
+            for k in np.unique(cu):
+                idx = np.where(cu == k)[0]
+                o = idx[np.argsort(st[idx, 0])]
+                per_cu[int(k)] = len(o)
+                if len(o) > 1:
+                    gaps.append(st[o[1:], 0] - st[o[:-1], 3])
+            g = np.concatenate(gaps) if gaps else np.zeros(1)
+            print(json.dumps({"cu_timeline": {"cus_seen": len(per_cu), "blocks_per_cu_med": med(list(per_cu.values())),
+                                              "gap_cyc_med": med(g), "gap_cyc_p90": float(np.percentile(g, 90)),
+                                              "gap_cyc_min": float(g.min())}}), flush=True)
+            return  # the stamps build overwrites candidate slots: nothing after this is meaningful
         t_rank = timed(lambda: mfma(hi, lo))
         ncand = int(ws.count[0].item())
         t_fix = timed(fix) if not os.environ.get("KB_NOFIX") else float("nan")  # diagnostic builds: garbage pairs
