@@ -136,6 +136,24 @@ __host__ __device__ __forceinline__ double score_error_bound(double ea, double e
   return ea + (1.0 + ea) * eb + gamma * (1.0 + ea) * (1.0 + eb) + 1e-12;
 }
 
+// Undecided-pair buffer layout (cand, cap uint64 entries), derived from the gallery set alone:
+//   cand[0, nb)                       per-bucket pair counters
+//   cand[nb + b*cap_b, +cap_b)        bucket b: pairs whose gallery row j has j >> 8 == b
+// Bucketing by 256 gallery rows lets the fix-up re-score a bucket's pairs while its 1 MiB of raw
+// gallery rows sits in one XCD's L2 (each gallery row has ~10 pairs): the gallery side is read from
+// HBM once instead of once per pair.
+constexpr int CAND_BUCKET_SHIFT = 8;
+struct CandLayout {
+  int64_t nb, cap_b;
+};
+inline CandLayout cand_layout(int64_t g_n_pad, int64_t cap) {
+  CandLayout l;
+  l.nb = std::max<int64_t>(1, (g_n_pad + (1 << CAND_BUCKET_SHIFT) - 1) >> CAND_BUCKET_SHIFT);
+  l.cap_b = cap > l.nb ? (cap - l.nb) / l.nb : 0;
+  return l;
+}
+constexpr int64_t FIXUP_MAX_BUCKETS_PER_XCD = 4096;  // LDS prefix of the XCD-ordered fix-up
+
 // per-row error plane and err_max slot of a sim mode (err_max = {hi, hilo, h16})
 inline const float* mode_err(const cmve_rows_t* r, int mode) {
   return mode == CMVE_SIM_BF16 ? r->err_hi : (mode == CMVE_SIM_BF16X3 ? r->err_hilo : r->err_h16);

@@ -81,6 +81,52 @@ __global__ __launch_bounds__(256) void thr_from_sgt_kernel(const double* __restr
   thr_lo[row] = f32_round_down(s - E);
 }
 
+// *cand_count = total pairs, or -- if a bucket outgrew cap_b (or cand is NULL: the buffer cannot
+// hold the counters) -- a size > cand_cap that fits the largest bucket, so the caller's
+// grow-and-retry allocates enough.
+__global__ __launch_bounds__(256) void cand_finalize_kernel(const uint64_t* __restrict__ bcnt, int64_t nb,
+                                                            int64_t cap_b, int64_t cap, int64_t* __restrict__ out) {
+  __shared__ unsigned long long s_tot[4], s_max[4];
+  unsigned long long tot = 0, mx = 0;
+  if (bcnt)
+    for (int64_t b = threadIdx.x; b < nb; b += 256) {
+      const unsigned long long c = bcnt[b];
+      tot += c;
+      mx = c > mx ? c : mx;
+    }
+  for (int o = 32; o >= 1; o >>= 1) {
+    tot += __shfl_xor(tot, o, 64);
+    const unsigned long long m2 = __shfl_xor(mx, o, 64);
+    mx = m2 > mx ? m2 : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_tot[threadIdx.x >> 6] = tot;
+    s_max[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tot = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+    mx = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+    if (!bcnt || (int64_t)mx > cap_b) {
+      const int64_t need = ((int64_t)mx + 1) * nb + nb + 1;
+      *out = need > cap ? need : cap + 1;
+    } else {
+      *out = (int64_t)tot;
+    }
+  }
+}
+
+int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* cand, int64_t cand_cap,
+                         int64_t* cand_count) {
+  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  hipLaunchKernelGGL(cand_finalize_kernel, dim3(1), dim3(256), 0, stream, (const uint64_t*)cand, l.nb, l.cap_b,
+                     cand_cap, cand_count);
+  return check_launch("cand_finalize");
+}
+
+// XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
+// x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
+// on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -88,13 +134,35 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t cap, const int64_t* __restrict__ cand_count) {
-  const int lane = threadIdx.x & 63;
-  const int64_t total = *cand_count;
-  const int64_t n = total < cap ? total : cap;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += stride) {
-    const uint64_t u = cand[c];
+                                                    int64_t nb, int64_t cap_b) {
+  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int xcd = blockIdx.x & 7;
+  const int64_t nk = xcd < nb ? (nb - xcd + 7) / 8 : 0;
+  if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
+    const int64_t per = (nk + 63) / 64;
+    const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
+    int64_t sum = 0;
+    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + 8 * k], cap_b);
+    int64_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int64_t run = incl - sum;
+    for (int64_t k = k0; k < k1; ++k) {
+      pre[k] = run;
+      run += min((int64_t)cand[xcd + 8 * k], cap_b);
+    }
+    if (lane == 63) pre[nk] = incl;
+  }
+  __syncthreads();
+  const int64_t total = pre[nk];
+  const int64_t stride = (int64_t)(gridDim.x >> 3) * 4;
+  int64_t k = 0;
+  for (int64_t c = (int64_t)(blockIdx.x >> 3) * 4 + wave; c < total; c += stride) {
+    while (pre[k + 1] <= c) ++k;
+    const uint64_t u = cand[nb + (xcd + 8 * k) * cap_b + (c - pre[k])];
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     const uint32_t flags = (uint32_t)(u >> 62);
@@ -109,14 +177,19 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
 int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs, const double* row_sgt,
                  const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t cand_cap,
                  const int64_t* cand_count) {
-  if (cand_cap == 0) return CMVE_OK;
-  const unsigned blocks = (unsigned)std::min<int64_t>(4096, (cand_cap + 3) / 4);
+  (void)cand_count;  // the bucket counters at the head of `cand` carry the sizes
+  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  if (l.cap_b == 0) return CMVE_OK;  // reported as overflow by the MFMA pass: the caller retries
+  CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "cmve_rank_fixup: gallery set too large (%lld buckets)",
+               (long long)l.nb);
+  // 128 blocks (512 waves) per XCD
+  const unsigned blocks = 8u * 128u;
   // a disabled direction has flags that never set its bit; pass its (possibly NULL) arrays through
   (void)dirs;
 #define FIX(TQ, TG)                                                                                                    \
   hipLaunchKernelGGL((fixup_kernel<TQ, TG>), dim3(blocks), dim3(256), 0, stream, (const TQ*)q->raw, q->raw_ld,        \
                      q->inv_norm, (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt, col_cnt, \
-                     cand, cand_cap, cand_count)
+                     cand, l.nb, l.cap_b)
   if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) FIX(float, float);
   else if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F64) FIX(float, double);
   else if (q->raw_dtype == CMVE_F64 && g->raw_dtype == CMVE_F32) FIX(double, float);

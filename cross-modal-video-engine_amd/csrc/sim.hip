@@ -59,9 +59,11 @@ struct SimArgs {
   const float* col_lo;
   int* row_cnt;
   int* col_cnt;
-  unsigned long long* cand;
+  unsigned long long* cand;        // bucket storage (cand_layout): bucket b at cand + b * cap_b
   long long cand_cap;
   unsigned long long* cand_count;
+  unsigned long long* bucket_cnt;  // per-bucket pair counters (head of the caller's buffer)
+  long long cap_b;
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
@@ -170,7 +172,7 @@ constexpr size_t stage_bytes() {
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
 #define CMVE_STAMP(k) \
-  if (threadIdx.x == 0) a.cand[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime()
+  if (threadIdx.x == 0) a.bucket_cnt[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else
 #define CMVE_STAMP(k)
 #endif
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   CMVE_STAMP(0);
 #ifdef CMVE_DBG_STAMPS  // where the block ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4)
   if (threadIdx.x == 0)
-    a.cand[(size_t)blockIdx.x * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+    a.bucket_cnt[(size_t)blockIdx.x * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                                           (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
   using G = Geo<WM, WN, TM>;
@@ -674,9 +676,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
                                             ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
           if (base < (uint32_t)CAND_LDS) {
             lds_cand[base] = packed;
-          } else {  // block buffer full: straight to the global list
-            const unsigned long long slot = atomicAdd(a.cand_count, 1ull);
-            if ((long long)slot < a.cand_cap) a.cand[slot] = packed;
+          } else {  // block buffer full: straight to the tile's bucket
+            const unsigned long long slot = atomicAdd(a.bucket_cnt + (n0 >> CAND_BUCKET_SHIFT), 1ull);
+            if ((long long)slot < a.cap_b) a.cand[(size_t)(n0 >> CAND_BUCKET_SHIFT) * a.cap_b + slot] = packed;
           }
           ++base;
         }
@@ -686,11 +688,12 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     __syncthreads();
     // flush the block's undecided pairs with ONE global atomic
     const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
-    if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.cand_count, (unsigned long long)nlds);
+    const int bucket = n0 >> CAND_BUCKET_SHIFT;  // a tile never straddles buckets (BN <= 256)
+    if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)nlds);
     __syncthreads();
     for (unsigned t = tid; t < nlds; t += NT) {
       const unsigned long long slot = *lds_cand_base + t;
-      if ((long long)slot < a.cand_cap) a.cand[slot] = lds_cand[t];
+      if ((long long)slot < a.cap_b) a.cand[(size_t)bucket * a.cap_b + slot] = lds_cand[t];
     }
     for (int t = tid; t < BM + BN; t += NT) {
       const int c = lds_rc[t];
@@ -809,9 +812,21 @@ extern "C" int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_
 
 // defined in rank.hip
 namespace cmve {
+int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* cand, int64_t cand_cap,
+                         int64_t* cand_count);
 int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs, const double* row_sgt,
                  const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t cand_cap,
                  const int64_t* cand_count);
+}
+
+// point the epilogue at the bucketed layout of `cand` (cand_layout) for the gallery view g
+static void set_cand(SimArgs& a, const cmve_rows_t* g, uint64_t* cand, int64_t cand_cap, int64_t* cand_count) {
+  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  a.bucket_cnt = (unsigned long long*)cand;
+  a.cand = (unsigned long long*)(cand + l.nb);
+  a.cap_b = l.cap_b;
+  a.cand_cap = cand_cap;
+  a.cand_count = (unsigned long long*)cand_count;
 }
 
 static int rank_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs, const float* row_hi,
@@ -834,10 +849,20 @@ static int rank_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, i
     a.col_lo = col_lo;
     a.col_cnt = col_cnt;
   }
-  a.cand = (unsigned long long*)cand;
-  a.cand_cap = cand_cap;
-  a.cand_count = (unsigned long long*)cand_count;
+  set_cand(a, g, cand, cand_cap, cand_count);
   return CMVE_OK;
+}
+
+// zero the bucket counters, run the rank GEMM, then write the pair total (or an overflow size) to
+// *cand_count.  A buffer too small for the bucket counters is reported as overflow untouched.
+static int rank_pass(const SimArgs& a, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, uint64_t* cand,
+                     int64_t cand_cap, int64_t* cand_count, hipStream_t s) {
+  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  if (l.cap_b == 0) return launch_cand_finalize(s, g, nullptr, cand_cap, cand_count);
+  CMVE_HIP(hipMemsetAsync(cand, 0, sizeof(uint64_t) * l.nb, s));
+  int st = dispatch<EPI_RANK>(a, q, g, mode, s);
+  if (st) return st;
+  return launch_cand_finalize(s, g, cand, cand_cap, cand_count);
 }
 
 extern "C" int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs,
@@ -853,7 +878,7 @@ extern "C" int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_
   if (dirs & CMVE_DIR_ROW) CMVE_HIP(hipMemsetAsync(row_cnt, 0, sizeof(int32_t) * q->n_pad, h->stream));
   if (dirs & CMVE_DIR_COL) CMVE_HIP(hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * g->n_pad, h->stream));
   if (q->n == 0 || g->n == 0) return CMVE_OK;
-  return dispatch<EPI_RANK>(a, q, g, mode, h->stream);
+  return rank_pass(a, q, g, mode, cand, cand_cap, cand_count, h->stream);
 }
 
 extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
@@ -957,11 +982,9 @@ extern "C" int cmve_rank_count_overlap(cmve_handle_t h, const cmve_rows_t* q, co
       ac.col_lo = col_lo + r0;
       ac.col_cnt = col_cnt + r0;
     }
-    ac.cand = (unsigned long long*)(cand + c * cap_c);
-    ac.cand_cap = cap_c;
-    ac.cand_count = (unsigned long long*)(cand_count + c);
+    set_cand(ac, &v, cand + c * cap_c, cap_c, cand_count + c);
     CMVE_HIP(hipEventRecord(h->tev[2 * c], s0));
-    st = dispatch<EPI_RANK>(ac, q, &v, mode, s0);
+    st = rank_pass(ac, q, &v, mode, cand + c * cap_c, cap_c, cand_count + c, s0);
     if (st) return st;
     CMVE_HIP(hipEventRecord(h->tev[2 * c + 1], s0));
     CMVE_HIP(hipEventRecord(h->ev[1 + c], s0));
