@@ -172,19 +172,17 @@ constexpr size_t stage_bytes() {
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
 #define CMVE_STAMP(k) \
-  if (threadIdx.x == 0) a.bucket_cnt[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime()
+  if (threadIdx.x == 0) a.bucket_cnt[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else
 #define CMVE_STAMP(k)
 #endif
 
+// Barrier for LDS hand-offs only: unlike __syncthreads it does not drain vmcnt, so loads issued
+// for the next tile stay in flight across the epilogue's barriers.
+#define CMVE_BAR_LDS() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
-  CMVE_STAMP(0);
-#ifdef CMVE_DBG_STAMPS  // where the block ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4)
-  if (threadIdx.x == 0)
-    a.bucket_cnt[(size_t)blockIdx.x * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-                                          (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-#endif
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -195,9 +193,24 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
   const int wr = wave / WN, wc = wave % WN;
-  int bm, bn;
-  tile_of_block(blockIdx.x, a.nblk_m, a.nblk_n, a.gn, bm, bn);
-  const int m0 = bm * BM, n0 = bn * BN;
+  // tiles: the phased (G256) kernel is persistent -- one block per CU walks tile, tile + gridDim.x,
+  // ... (same XCD, same XCD-local order as a one-tile-per-block grid); the G128 grid is one tile each
+  const int ntiles = a.nblk_m * a.nblk_n;
+  int tile = blockIdx.x;
+  int m0, n0;
+  auto tile_origin = [&](int t, int& mo, int& no) {
+    int bm_, bn_;
+    tile_of_block(t, a.nblk_m, a.nblk_n, a.gn, bm_, bn_);
+    mo = bm_ * BM;
+    no = bn_ * BN;
+  };
+  tile_origin(tile, m0, n0);
+  CMVE_STAMP(0);
+#ifdef CMVE_DBG_STAMPS  // where the block ran: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4)
+  if (threadIdx.x == 0)
+    a.bucket_cnt[(size_t)tile * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                         (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
 
   // epilogue scratch after the staging buffers (one dynamic LDS object only)
   int* lds_rc = (int*)(smem + 2 * STAGE_BYTES);
@@ -208,21 +221,25 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   // rank thresholds of the tile: [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
   float* lds_thr = (float*)(lds_cand_base + 1);
   float thr_hi_v = __builtin_nanf(""), thr_lo_v = __builtin_nanf("");
-  if constexpr (EPI == EPI_RANK) {
-    static_assert(NT == BM + BN, "one threshold pair per thread");
-    for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
-    if (tid == 0) *lds_ncand = 0u;
-    // fetched now, published to LDS after the main loop: the epilogue must not wait on HBM
-    // (8 dependent threshold loads per wave inside it cost ~28% of the kernel)
+  // a tile's thresholds are fetched when its loads are issued and published to LDS in its
+  // epilogue: the epilogue must not wait on HBM (8 dependent loads per wave there cost ~28%)
+  auto fetch_thr = [&](int mo, int no, float& hi, float& lo) {
+    hi = lo = __builtin_nanf("");
     if (tid < BM) {
       if (a.row_hi) {
-        thr_hi_v = a.row_hi[m0 + tid];
-        thr_lo_v = a.row_lo[m0 + tid];
+        hi = a.row_hi[mo + tid];
+        lo = a.row_lo[mo + tid];
       }
     } else if (a.col_hi) {
-      thr_hi_v = a.col_hi[n0 + tid - BM];
-      thr_lo_v = a.col_lo[n0 + tid - BM];
+      hi = a.col_hi[no + tid - BM];
+      lo = a.col_lo[no + tid - BM];
     }
+  };
+  if constexpr (EPI == EPI_RANK) {
+    static_assert(NT == BM + BN, "one threshold pair per thread");
+    for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
+    if (tid == 0) *lds_ncand = 0u;
+    fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
   }
 
   auto stage = [&](int t, int s) {
@@ -245,6 +262,269 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  auto epilogue = [&]() {
+  #ifdef CMVE_DBG_NOEPI  // diagnostic build only: main loop without any epilogue (results are garbage)
+  #pragma unroll
+    for (int i = 0; i < TM; ++i)
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  #endif
+    // ---------------- epilogues ----------------
+    // accumulator element (i, j, r): row = m0 + wr*TM*16 + i*16 + (lane>>4)*4 + r,
+    //                                col = n0 + wc*TN*16 + j*16 + (lane&15)
+    const int rbase = m0 + wr * (TM * 16) + (lane >> 4) * 4;
+    const int cbase = n0 + wc * (TN * 16) + (lane & 15);
+
+    if constexpr (EPI == EPI_LINEAR) {
+      float bj[TN], sj[TN], hj[TN];
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = cbase + j * 16;
+        const bool ok = col < a.ng;
+        bj[j] = (a.bias && ok) ? a.bias[col] : 0.f;
+        sj[j] = (a.bn_scale && ok) ? a.bn_scale[col] : 1.f;
+        hj[j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
+      }
+  #pragma unroll
+      for (int i = 0; i < TM; ++i)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + i * 16 + r;
+          if (row >= a.nq) continue;
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 16;
+            if (col >= a.ng) continue;
+            float v = acc[i][j][r] + bj[j];
+            if (a.relu == 1) v = fmaxf(v, 0.f);                         // ReLU
+            else if (a.relu == 2) v = v / (1.f + expf(-1.702f * v));  // QuickGELU x*sigmoid(1.702x)
+            else if (a.relu == 3) v = 1.f / (1.f + expf(-v));         // Sigmoid
+            if (a.resid) v = a.resid[(int64_t)row * a.ldr + col] + v;
+            if (a.bn_scale) v = v * sj[j] + hj[j];
+            ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
+          }
+        }
+    } else if constexpr (EPI == EPI_STORE) {
+  #pragma unroll
+      for (int i = 0; i < TM; ++i)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + i * 16 + r;
+          if (row >= a.nq) continue;
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 16;
+            if (col >= a.ng) continue;
+            const float v = a.alpha * acc[i][j][r] + a.beta;
+            if (a.out_f64)
+              ((double*)a.out)[(int64_t)row * a.ldo + col] = (double)v;
+            else
+              ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
+          }
+        }
+    } else {
+      // thresholds from LDS; a disabled direction holds NaN, which no comparison passes (not even s = +inf)
+      lds_thr[tid] = thr_hi_v;
+      lds_thr[NT + tid] = thr_lo_v;
+      CMVE_BAR_LDS();
+      CMVE_STAMP(4);
+      const float* l_rhi = lds_thr + (rbase - m0);
+      const float* l_rlo = lds_thr + NT + (rbase - m0);
+      float chi[TN], clo[TN];
+  #pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        chi[j] = lds_thr[BM + (cbase - n0) + j * 16];
+        clo[j] = lds_thr[NT + BM + (cbase - n0) + j * 16];
+      }
+      // Branch-free scoring pass: per score only compares and bit packing.  Undecided pairs are
+      // recorded as bits (per i: bit j*4+r = row-undecided, bit 16+j*4+r = column-undecided) and
+      // emitted afterwards with ONE LDS atomic per wave; a per-score atomic with exec-mask
+      // branches cost ~40% of the block (s_memtime stamps, tools/kbench.py KB_STAMPS).
+      const bool padded = (m0 + BM > a.nq) || (n0 + BN > a.ng);
+      uint32_t rowok = 0xffffffffu, colok = 0xfu;  // bit i*4+r / bit j: inside the real n_q x n_g
+      if (padded) {
+        rowok = 0u;
+        colok = 0u;
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) rowok |= (uint32_t)(rbase + i * 16 + r < a.nq) << (i * 4 + r);
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) colok |= (uint32_t)(cbase + j * 16 < a.ng) << j;
+      }
+      uint32_t cc_pack = 0u;  // byte j: count for column j (<= 4*TM per lane, <= 16*TM after the reduce)
+      uint32_t und[TM];
+      // exact undecided bits of one i-block: lo <= s <= hi from its own compares (reusing
+      // "!(s > hi)" kept 128 lane masks live and spilled them); a disabled direction is skipped
+      auto und_bits = [&](int i, const f32x4_t& rhi, const f32x4_t& rlo, bool dr, bool dc) {
+        uint32_t u = 0u;
+  #pragma unroll
+        for (int j = 0; j < TN; ++j)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sc = acc[i][j][r];
+            if (dr) u |= ((sc >= rlo[r] && sc <= rhi[r]) ? 1u : 0u) << (j * 4 + r);
+            if (dc) u |= ((sc >= clo[j] && sc <= chi[j]) ? 1u : 0u) << (16 + j * 4 + r);
+          }
+        return u;
+      };
+      auto row_reduce = [&](int i, uint32_t rc_pack) {
+        // rows: sum over the 16 lanes of a DPP row (those sharing lane >> 4); bytes stay <= 64
+        rc_pack = row_sum16(rc_pack);
+        if ((lane & 15) == 0) {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t c = (rc_pack >> (8 * r)) & 0xffu;
+            if (c) atomicAdd(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
+          }
+        }
+      };
+      const bool do_row = a.row_hi != nullptr, do_col = a.col_hi != nullptr;
+      // fast scoring of an unpadded tile: per score an exact count compare (v_cmp + v_addc) and an
+      // "inside [lo, hi]" test (v_med3 + v_cmp) folded into a wave mask; the exact undecided bits
+      // are recomputed only for i-blocks where some lane hit.  The epilogue is VALU-issue-bound
+      // (4 cycles per wave64 instruction x 128 scores per lane): every instruction per score counts.
+      auto fast_block = [&](auto row_c, auto col_c) {
+        constexpr bool DR = decltype(row_c)::value, DC = decltype(col_c)::value;
+        uint32_t ccnt[TN] = {};
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          __builtin_amdgcn_sched_barrier(0);
+          f32x4_t rhi = {}, rlo = {};
+          if constexpr (DR) {
+            rhi = *(const f32x4_t*)(l_rhi + i * 16);
+            rlo = *(const f32x4_t*)(l_rlo + i * 16);
+          }
+          uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
+          bool hit = false;
+          if constexpr (DR && !DC && TN == 4) {  // the bench / t2v shape: hand-scheduled per row
+            unsigned long long hm = 0ull;
+            c0 = row4_count_hit(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], hm);
+            c1 = row4_count_hit(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], hm);
+            c2 = row4_count_hit(acc[i][0][2], acc[i][1][2], acc[i][2][2], acc[i][3][2], rhi[2], rlo[2], hm);
+            c3 = row4_count_hit(acc[i][0][3], acc[i][1][3], acc[i][2][3], acc[i][3][3], rhi[3], rlo[3], hm);
+            hit = hm != 0ull;  // wave-uniform
+          } else
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const f32x4_t sc = acc[i][j];
+            if constexpr (DR) {
+              c0 += sc[0] > rhi[0];
+              c1 += sc[1] > rhi[1];
+              c2 += sc[2] > rhi[2];
+              c3 += sc[3] > rhi[3];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) hit |= __builtin_amdgcn_fmed3f(sc[r], rlo[r], rhi[r]) == sc[r];
+            }
+            if constexpr (DC) {
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ccnt[j] += sc[r] > chi[j];
+                hit |= __builtin_amdgcn_fmed3f(sc[r], clo[j], chi[j]) == sc[r];
+              }
+            }
+          }
+          if constexpr (DR) row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+          und[i] = __builtin_amdgcn_ballot_w64(hit) ? und_bits(i, rhi, rlo, DR, DC) : 0u;
+        }
+        if constexpr (DC) {
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) cc_pack += ccnt[j] << (8 * j);
+        }
+      };
+      if (padded) {  // boundary tiles: out-of-range scores -> -inf (never counted, never in a band)
+              for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (!((rowok >> (i * 4 + r)) & (colok >> j) & 1u)) acc[i][j][r] = -INFINITY;
+      }
+      if (do_row && do_col) {
+        fast_block(std::true_type{}, std::true_type{});
+      } else if (do_row) {
+        fast_block(std::true_type{}, std::false_type{});
+      } else {
+        fast_block(std::false_type{}, std::true_type{});
+      }
+      cc_pack += __shfl_xor(cc_pack, 16, 64);
+      cc_pack += __shfl_xor(cc_pack, 32, 64);
+      if (lane < 16) {
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const uint32_t c = (cc_pack >> (8 * j)) & 0xffu;
+          if (c) atomicAdd(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
+        }
+      }
+      CMVE_STAMP(5);
+      // emission: wave-inclusive scan of the per-lane counts, one LDS atomic per wave
+      uint32_t nmine = 0u;
+  #pragma unroll
+      for (int i = 0; i < TM; ++i) nmine += __builtin_popcount((und[i] | (und[i] >> 16)) & 0xffffu);
+      // exclusive prefix of nmine over lanes from one ballot per count bit (mbcnt = popcount of
+      // the lower lanes); nmine <= 16*TM < 256.  No LDS round trips (a __shfl scan is 6 bpermutes).
+      uint32_t excl = 0u, total = 0u;
+      if (__builtin_amdgcn_ballot_w64(nmine != 0u)) {
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const unsigned long long m = __builtin_amdgcn_ballot_w64((nmine >> b) & 1u);
+          excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+          total += (uint32_t)__builtin_popcountll(m) << b;
+        }
+      }
+      if (total) {
+        uint32_t base = 0u;
+        if (lane == 0) base = atomicAdd(lds_ncand, total);
+        base = __builtin_amdgcn_readfirstlane(base) + excl;
+  #pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          uint32_t m = (und[i] | (und[i] >> 16)) & 0xffffu;
+          while (m) {
+            const int bit = __builtin_ctz(m);
+            m &= m - 1u;
+            const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
+            const unsigned long long packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
+                                              ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
+            if (base < (uint32_t)CAND_LDS) {
+              lds_cand[base] = packed;
+            } else {  // block buffer full: straight to the tile's bucket
+              const unsigned long long slot = atomicAdd(a.bucket_cnt + (n0 >> CAND_BUCKET_SHIFT), 1ull);
+              if ((long long)slot < a.cap_b) a.cand[(size_t)(n0 >> CAND_BUCKET_SHIFT) * a.cap_b + slot] = packed;
+            }
+            ++base;
+          }
+        }
+      }
+      CMVE_STAMP(6);
+      CMVE_BAR_LDS();
+      // flush the block's undecided pairs with ONE global atomic
+      const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
+      const int bucket = n0 >> CAND_BUCKET_SHIFT;  // a tile never straddles buckets (BN <= 256)
+      if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)nlds);
+      CMVE_BAR_LDS();
+      for (unsigned t = tid; t < nlds; t += NT) {
+        const unsigned long long slot = *lds_cand_base + t;
+        if ((long long)slot < a.cap_b) a.cand[(size_t)bucket * a.cap_b + slot] = lds_cand[t];
+      }
+      if (tid == 0) *lds_ncand = 0u;  // every thread read it before the barrier above
+      for (int t = tid; t < BM + BN; t += NT) {
+        const int c = lds_rc[t];
+        lds_rc[t] = 0;  // owner thread: ready for the next tile
+        if (!c) continue;
+        if (t < BM) {
+          if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
+        } else {
+          if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
+        }
+      }
+  #ifdef CMVE_DBG_STAMPS
+      CMVE_BAR_LDS();
+  #endif
+      CMVE_STAMP(3);
+    }
+  };
+
   const int frow = lane & 15;
   if constexpr (PHASED) {
     // ---- G256 phased schedule (2 buffers of BK=64, 4 phases per K-tile, 2 staggered groups) ----
@@ -261,10 +541,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     // WAR: a buffer is restaged >= 2 phases after its last ds_read (cdna_hip_programming.md Sec.5).
     static_assert(BM == 256 && BN == 256 && TM == 8 && TN == 4 && NW == 8, "phased path is the 256x256 geometry");
     const int ldk_b = (int)(a.ldk * 2);
-    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.qhi + (int64_t)m0 * a.ldk), 0, BM * ldk_b, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.ghi + (int64_t)n0 * a.ldk), 0, BN * ldk_b, 0x00020000);
+    auto rsrc_of = [&](const uint16_t* base, int row0, int rows) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (int64_t)row0 * a.ldk), 0, rows * ldk_b, 0x00020000);
+    };
+    __amdgpu_buffer_rsrc_t rA = rsrc_of(a.qhi, m0, BM);
+    __amdgpu_buffer_rsrc_t rB = rsrc_of(a.ghi, n0, BN);
     // piece = 8 rows x 128 B (one wave-instruction, 1 KiB): lane l -> row l>>3, LDS chunk l&7,
     // global chunk (l&7) ^ (row&7)
     const int voff = (lane >> 3) * ldk_b + (((lane & 7) ^ (lane >> 3)) << 4);
@@ -325,15 +606,16 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   asm volatile("s_barrier" ::: "memory");           \
   __builtin_amdgcn_sched_barrier(0)
 
-    // prologue: K-tile 0 (A, B) and B(1); wait for K-tile 0
-    stage_op(rA, 0, 0);
-    stage_op(rB, 0, A_BYTES);
-    if (nk > 1) {
-      stage_op(rB, 1, A_BYTES);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // a tile's first loads: K-tile 0 (A, B) and B(1).  For every tile after a block's first they
+    // are issued before the previous tile's epilogue, whose ~10k cycles hide their latency.
+    auto prologue_loads = [&]() {
+      stage_op(rA, 0, 0);
+      stage_op(rB, 0, A_BYTES);
+      if (nk > 1) stage_op(rB, 1, A_BYTES);
+    };
+    prologue_loads();
+    for (;;) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     CMVE_BAR();
     CMVE_STAMP(1);
     if (wr == 1) { CMVE_BAR(); }  // stagger: group 1 runs one barrier behind
@@ -369,6 +651,31 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     }
     if (wr == 0) { CMVE_BAR(); }  // re-align the barrier counts of the two groups
     CMVE_STAMP(2);
+    // every K-tile of this tile has been read (both groups passed the realigning barrier): the
+    // staging buffers are free for the next tile while this one's epilogue runs
+    const int next = tile + (int)gridDim.x;
+    const bool has_next = next < ntiles;
+    int m0n = 0, n0n = 0;
+    float thn_hi = 0.f, thn_lo = 0.f;
+    if (has_next) {
+      tile_origin(next, m0n, n0n);
+      rA = rsrc_of(a.qhi, m0n, BM);
+      rB = rsrc_of(a.ghi, n0n, BN);
+      prologue_loads();
+      if constexpr (EPI == EPI_RANK) fetch_thr(m0n, n0n, thn_hi, thn_lo);
+    }
+    epilogue();
+    if (!has_next) break;
+    tile = next;
+    m0 = m0n;
+    n0 = n0n;
+    thr_hi_v = thn_hi;
+    thr_lo_v = thn_lo;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
 #undef CMVE_BAR
   } else {
   stage(0, 0);
@@ -438,277 +745,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   }
   }
 
-#ifdef CMVE_DBG_NOEPI  // diagnostic build only: main loop without any epilogue (results are garbage)
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-  return;
-#endif
-  // ---------------- epilogues ----------------
-  // accumulator element (i, j, r): row = m0 + wr*TM*16 + i*16 + (lane>>4)*4 + r,
-  //                                col = n0 + wc*TN*16 + j*16 + (lane&15)
-  const int rbase = m0 + wr * (TM * 16) + (lane >> 4) * 4;
-  const int cbase = n0 + wc * (TN * 16) + (lane & 15);
-
-  if constexpr (EPI == EPI_LINEAR) {
-    float bj[TN], sj[TN], hj[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = cbase + j * 16;
-      const bool ok = col < a.ng;
-      bj[j] = (a.bias && ok) ? a.bias[col] : 0.f;
-      sj[j] = (a.bn_scale && ok) ? a.bn_scale[col] : 1.f;
-      hj[j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + r;
-        if (row >= a.nq) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = cbase + j * 16;
-          if (col >= a.ng) continue;
-          float v = acc[i][j][r] + bj[j];
-          if (a.relu == 1) v = fmaxf(v, 0.f);                         // ReLU
-          else if (a.relu == 2) v = v / (1.f + expf(-1.702f * v));  // QuickGELU x*sigmoid(1.702x)
-          else if (a.relu == 3) v = 1.f / (1.f + expf(-v));         // Sigmoid
-          if (a.resid) v = a.resid[(int64_t)row * a.ldr + col] + v;
-          if (a.bn_scale) v = v * sj[j] + hj[j];
-          ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
-        }
-      }
-  } else if constexpr (EPI == EPI_STORE) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + r;
-        if (row >= a.nq) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = cbase + j * 16;
-          if (col >= a.ng) continue;
-          const float v = a.alpha * acc[i][j][r] + a.beta;
-          if (a.out_f64)
-            ((double*)a.out)[(int64_t)row * a.ldo + col] = (double)v;
-          else
-            ((float*)a.out)[(int64_t)row * a.ldo + col] = v;
-        }
-      }
-  } else {
-    // thresholds from LDS; a disabled direction holds NaN, which no comparison passes (not even s = +inf)
-    lds_thr[tid] = thr_hi_v;
-    lds_thr[NT + tid] = thr_lo_v;
-    __syncthreads();
-    CMVE_STAMP(4);
-    const float* l_rhi = lds_thr + (rbase - m0);
-    const float* l_rlo = lds_thr + NT + (rbase - m0);
-    float chi[TN], clo[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      chi[j] = lds_thr[BM + (cbase - n0) + j * 16];
-      clo[j] = lds_thr[NT + BM + (cbase - n0) + j * 16];
-    }
-    // Branch-free scoring pass: per score only compares and bit packing.  Undecided pairs are
-    // recorded as bits (per i: bit j*4+r = row-undecided, bit 16+j*4+r = column-undecided) and
-    // emitted afterwards with ONE LDS atomic per wave; a per-score atomic with exec-mask
-    // branches cost ~40% of the block (s_memtime stamps, tools/kbench.py KB_STAMPS).
-    const bool padded = (m0 + BM > a.nq) || (n0 + BN > a.ng);
-    uint32_t rowok = 0xffffffffu, colok = 0xfu;  // bit i*4+r / bit j: inside the real n_q x n_g
-    if (padded) {
-      rowok = 0u;
-      colok = 0u;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rowok |= (uint32_t)(rbase + i * 16 + r < a.nq) << (i * 4 + r);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) colok |= (uint32_t)(cbase + j * 16 < a.ng) << j;
-    }
-    uint32_t cc_pack = 0u;  // byte j: count for column j (<= 4*TM per lane, <= 16*TM after the reduce)
-    uint32_t und[TM];
-    // exact undecided bits of one i-block: lo <= s <= hi from its own compares (reusing
-    // "!(s > hi)" kept 128 lane masks live and spilled them); a disabled direction is skipped
-    auto und_bits = [&](int i, const f32x4_t& rhi, const f32x4_t& rlo, bool dr, bool dc, auto padded_c) {
-      constexpr bool PAD = decltype(padded_c)::value;
-      uint32_t u = 0u;
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float sc = acc[i][j][r];
-          if constexpr (PAD) sc = ((rowok >> (i * 4 + r)) & (colok >> j) & 1u) ? sc : -INFINITY;
-          if (dr) u |= ((sc >= rlo[r] && sc <= rhi[r]) ? 1u : 0u) << (j * 4 + r);
-          if (dc) u |= ((sc >= clo[j] && sc <= chi[j]) ? 1u : 0u) << (16 + j * 4 + r);
-        }
-      return u;
-    };
-    auto row_reduce = [&](int i, uint32_t rc_pack) {
-      // rows: sum over the 16 lanes of a DPP row (those sharing lane >> 4); bytes stay <= 64
-      rc_pack = row_sum16(rc_pack);
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t c = (rc_pack >> (8 * r)) & 0xffu;
-          if (c) atomicAdd(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
-        }
-      }
-    };
-    const bool do_row = a.row_hi != nullptr, do_col = a.col_hi != nullptr;
-    // fast scoring of an unpadded tile: per score an exact count compare (v_cmp + v_addc) and an
-    // "inside [lo, hi]" test (v_med3 + v_cmp) folded into a wave mask; the exact undecided bits
-    // are recomputed only for i-blocks where some lane hit.  The epilogue is VALU-issue-bound
-    // (4 cycles per wave64 instruction x 128 scores per lane): every instruction per score counts.
-    auto fast_block = [&](auto row_c, auto col_c) {
-      constexpr bool DR = decltype(row_c)::value, DC = decltype(col_c)::value;
-      uint32_t ccnt[TN] = {};
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4_t rhi = {}, rlo = {};
-        if constexpr (DR) {
-          rhi = *(const f32x4_t*)(l_rhi + i * 16);
-          rlo = *(const f32x4_t*)(l_rlo + i * 16);
-        }
-        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
-        bool hit = false;
-        if constexpr (DR && !DC && TN == 4) {  // the bench / t2v shape: hand-scheduled per row
-          unsigned long long hm = 0ull;
-          c0 = row4_count_hit(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], hm);
-          c1 = row4_count_hit(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], hm);
-          c2 = row4_count_hit(acc[i][0][2], acc[i][1][2], acc[i][2][2], acc[i][3][2], rhi[2], rlo[2], hm);
-          c3 = row4_count_hit(acc[i][0][3], acc[i][1][3], acc[i][2][3], acc[i][3][3], rhi[3], rlo[3], hm);
-          hit = hm != 0ull;  // wave-uniform
-        } else
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const f32x4_t sc = acc[i][j];
-          if constexpr (DR) {
-            c0 += sc[0] > rhi[0];
-            c1 += sc[1] > rhi[1];
-            c2 += sc[2] > rhi[2];
-            c3 += sc[3] > rhi[3];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) hit |= __builtin_amdgcn_fmed3f(sc[r], rlo[r], rhi[r]) == sc[r];
-          }
-          if constexpr (DC) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              ccnt[j] += sc[r] > chi[j];
-              hit |= __builtin_amdgcn_fmed3f(sc[r], clo[j], chi[j]) == sc[r];
-            }
-          }
-        }
-        if constexpr (DR) row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
-        und[i] = __builtin_amdgcn_ballot_w64(hit) ? und_bits(i, rhi, rlo, DR, DC, std::false_type{}) : 0u;
-      }
-      if constexpr (DC) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) cc_pack += ccnt[j] << (8 * j);
-      }
-    };
-    if (padded) {  // boundary tiles: generic, masked
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
-        const f32x4_t rhi = *(const f32x4_t*)(l_rhi + i * 16);
-        const f32x4_t rlo = *(const f32x4_t*)(l_rlo + i * 16);
-        uint32_t rc_pack = 0u;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float sc = acc[i][j][r];
-            sc = ((rowok >> (i * 4 + r)) & (colok >> j) & 1u) ? sc : -INFINITY;
-            rc_pack += (sc > rhi[r] ? 1u : 0u) << (8 * r);
-            cc_pack += (sc > chi[j] ? 1u : 0u) << (8 * j);
-          }
-        und[i] = und_bits(i, rhi, rlo, do_row, do_col, std::true_type{});
-        row_reduce(i, rc_pack);
-      }
-    } else if (do_row && do_col) {
-      fast_block(std::true_type{}, std::true_type{});
-    } else if (do_row) {
-      fast_block(std::true_type{}, std::false_type{});
-    } else {
-      fast_block(std::false_type{}, std::true_type{});
-    }
-    cc_pack += __shfl_xor(cc_pack, 16, 64);
-    cc_pack += __shfl_xor(cc_pack, 32, 64);
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const uint32_t c = (cc_pack >> (8 * j)) & 0xffu;
-        if (c) atomicAdd(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
-      }
-    }
-    CMVE_STAMP(5);
-    // emission: wave-inclusive scan of the per-lane counts, one LDS atomic per wave
-    uint32_t nmine = 0u;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) nmine += __builtin_popcount((und[i] | (und[i] >> 16)) & 0xffffu);
-    // exclusive prefix of nmine over lanes from one ballot per count bit (mbcnt = popcount of
-    // the lower lanes); nmine <= 16*TM < 256.  No LDS round trips (a __shfl scan is 6 bpermutes).
-    uint32_t excl = 0u, total = 0u;
-    if (__builtin_amdgcn_ballot_w64(nmine != 0u)) {
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const unsigned long long m = __builtin_amdgcn_ballot_w64((nmine >> b) & 1u);
-        excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
-        total += (uint32_t)__builtin_popcountll(m) << b;
-      }
-    }
-    if (total) {
-      uint32_t base = 0u;
-      if (lane == 0) base = atomicAdd(lds_ncand, total);
-      base = __builtin_amdgcn_readfirstlane(base) + excl;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        uint32_t m = (und[i] | (und[i] >> 16)) & 0xffffu;
-        while (m) {
-          const int bit = __builtin_ctz(m);
-          m &= m - 1u;
-          const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
-          const unsigned long long packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
-                                            ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
-          if (base < (uint32_t)CAND_LDS) {
-            lds_cand[base] = packed;
-          } else {  // block buffer full: straight to the tile's bucket
-            const unsigned long long slot = atomicAdd(a.bucket_cnt + (n0 >> CAND_BUCKET_SHIFT), 1ull);
-            if ((long long)slot < a.cap_b) a.cand[(size_t)(n0 >> CAND_BUCKET_SHIFT) * a.cap_b + slot] = packed;
-          }
-          ++base;
-        }
-      }
-    }
-    CMVE_STAMP(6);
-    __syncthreads();
-    // flush the block's undecided pairs with ONE global atomic
-    const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
-    const int bucket = n0 >> CAND_BUCKET_SHIFT;  // a tile never straddles buckets (BN <= 256)
-    if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)nlds);
-    __syncthreads();
-    for (unsigned t = tid; t < nlds; t += NT) {
-      const unsigned long long slot = *lds_cand_base + t;
-      if ((long long)slot < a.cap_b) a.cand[(size_t)bucket * a.cap_b + slot] = lds_cand[t];
-    }
-    for (int t = tid; t < BM + BN; t += NT) {
-      const int c = lds_rc[t];
-      if (!c) continue;
-      if (t < BM) {
-        if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
-      } else {
-        if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
-      }
-    }
-#ifdef CMVE_DBG_STAMPS
-    __syncthreads();
-#endif
-    CMVE_STAMP(3);
-  }
+  if constexpr (!PHASED) epilogue();
 }
 
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
@@ -731,7 +768,17 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
     return e ? atoi(e) : 0;
   }();
   a.gn = gn_env > 0 ? gn_env : 8;
-  const unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
+  unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
+  if constexpr (PHASED) {  // persistent: one block per CU (a multiple of 8: the XCD map is blockIdx & 7)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      CMVE_HIP(hipGetDevice(&dev));
+      CMVE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      cus = std::max(8, cus / 8 * 8);
+    }
+    nblocks = std::min<unsigned>(nblocks, (unsigned)cus);
+  }
   hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, PHASED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
   return check_launch("sim_kernel");
 }
