@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="skip the 1kA and CPU legs (profiling runs)")
     p.add_argument("--chunks", type=int, default=1,
                    help="gallery pieces per shard: each piece's fp64 fix-up overlaps the next piece's MFMA pass")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_traffic.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
     return p.parse_args()
 
 

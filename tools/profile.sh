@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for the bench's dominant kernel (run on the GPU box via gpurun).
-#   pass 1: kernel trace + stats;  pass 2: FETCH_SIZE;  pass 3: WRITE_SIZE  (separate PMC passes)
+#   pass 1: kernel trace + stats;  pass 2: FETCH_SIZE;  pass 3: WRITE_SIZE;  pass 4: MFMA busy + clock
+#   (separate PMC passes)
 # then tools/traffic.py turns them into profiles/<tag>_traffic.json (read by bench.py).
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -12,5 +13,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$R/bench.py" $ARGS > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras > "$OUT/bench_write.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d "$OUT/mfma" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras > "$OUT/bench_mfma.log" 2>&1
 python3 "$R/tools/traffic.py" "$OUT" "$TAG" > "$OUT/traffic.log" 2>&1
 echo "profile done: $OUT"

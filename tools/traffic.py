@@ -44,6 +44,19 @@ def main(outdir, tag):
            "write_kib_per_launch": (sum(w) / len(w)) if w else None}
     if f and w:
         out["hbm_bytes_per_launch"] = 2 * out["fetch_kib_per_launch"] * 1024 + out["write_kib_per_launch"] * 1024
+    # MFMA pipe utilisation and effective clock of the same kernel (pass 4): SQ_VALU_MFMA_BUSY_CYCLES
+    # counts busy cycles summed over SIMDs; GRBM_GUI_ACTIVE / 8 XCDs / duration = effective clock
+    mf = {}
+    for r in rows(os.path.join(outdir, "mfma", "**", "*counter_collection.csv")):
+        name = r.get("Kernel_Name", "")
+        if "sim_kernel" in name and ("<2, 1" in name or "ILi2ELi1E" in name):
+            d = mf.setdefault(r["Dispatch_Id"], {"dur": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9})
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if mf:
+        last = [v for v in mf.values() if "GRBM_GUI_ACTIVE" in v and "SQ_VALU_MFMA_BUSY_CYCLES" in v][-1]
+        clk = last["GRBM_GUI_ACTIVE"] / 8 / last["dur"]
+        out["effective_clock_ghz"] = clk / 1e9
+        out["mfma_busy_frac"] = last["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * last["dur"] * 256 * 4)
     out.update({"shard": 131072, "nq": 16384, "dim": 1024, "chunks": 1,
                 "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"})
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
