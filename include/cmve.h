@@ -228,10 +228,13 @@ int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a_set, const cmve_row
  *   row_cnt[i] = #{ j : cos64(q_i, g_j) > row_sgt[i] }   (if CMVE_DIR_ROW in dirs)
  *   col_cnt[j] = #{ i : cos64(q_i, g_j) > col_sgt[j] }   (if CMVE_DIR_COL in dirs)
  * The MFMA pass counts the pairs that are certain under the error bound and
- * appends the undecided (i, j) pairs to `cand` (capacity cand_cap, uint64 each);
+ * files the undecided (i, j) pairs in `cand` (capacity cand_cap, uint64 each;
+ * its layout is internal to the library: per-bucket counters followed by buckets
+ * of 256 gallery rows, so the fix-up reads each gallery row from HBM once);
  * an fp64 fix-up kernel re-scores those exactly.  *cand_count (device int64)
  * receives the number of undecided pairs; if it exceeds cand_cap the counts are
- * incomplete and the caller must retry with a larger buffer.
+ * incomplete (a bucket overflowed) and the caller must retry with a buffer of at
+ * least *cand_count entries.
  * gt rank (1-based) = 1 + cnt, i.e. the position of the best GT in the reference's
  * np.argsort (LINAS-engine/util/metrics.py:137-147) on tie-free inputs.
  * row_cnt/col_cnt are zeroed by the call.
