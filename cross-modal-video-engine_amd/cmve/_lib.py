@@ -79,6 +79,10 @@ SIGNATURES = {
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_topk": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp]),
+    "cmve_bigfile_open": (C.c_int, [C.c_char_p, _i64, _i32, _P(_vp)]),
+    "cmve_bigfile_close": (C.c_int, [_vp]),
+    "cmve_bigfile_gather": (C.c_int, [_vp, _vp, _i64, _vp, _i32]),
+    "cmve_bigfile_gather_device": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _i32]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():

@@ -323,6 +323,24 @@ int cmve_gt_positions_from_matrix(cmve_handle_t h, const void* errors, int32_t d
 int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
               float* scores_ws, int32_t* out_idx, double* out_score, int32_t* overflow);
 
+/* ---- on-disk feature store -------------------------------
+ * BigFile: feature.bin = n_rows x dim float32, row-major (LINAS-engine/basic/bigfile.py:6-18).
+ * These are HOST calls (they read the page cache); the device variant also enqueues H2D copies on
+ * the handle's stream and waits only for its own staging halves.
+ * Replaces: BigFile.read / read_one (LINAS-engine/basic/bigfile.py:23-60), called once per
+ * frame by VisDataSet4DualEncoding.__getitem__ (LINAS-engine/util/tag_data_provider.py:330-337). */
+typedef struct cmve_bigfile* cmve_bigfile_t;
+/* map feature.bin read-only (validates its size against n_rows x dim) */
+int cmve_bigfile_open(const char* feature_bin, int64_t n_rows, int32_t dim, cmve_bigfile_t* out);
+int cmve_bigfile_close(cmve_bigfile_t bf);
+/* out[k, :] = row rows[k] (host arrays; `threads` memcpy workers); a row outside [0, n_rows) is an error */
+int cmve_bigfile_gather(cmve_bigfile_t bf, const int64_t* rows, int64_t n, float* out, int32_t threads);
+/* dst[k, :] (device) = row rows[k], streamed through `staging` (pinned host, staging_rows x dim
+ * floats, used as two halves: the H2D copy of one half overlaps the gather of the other).  staging
+ * must stay untouched until the handle's stream has passed this call. */
+int cmve_bigfile_gather_device(cmve_handle_t h, cmve_bigfile_t bf, const int64_t* rows, int64_t n, float* dst,
+                               float* staging, int64_t staging_rows, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -115,3 +115,35 @@ def combiner_inputs(b, seed, frames=8, tokens=16, d=640):
     text = rng.standard_normal((b, d), dtype=np.float32)
     tgt = rng.standard_normal((b, frames, d), dtype=np.float32)
     return high, mid, text, tgt
+
+
+def bigfile_toy(datadir, seed=21, n_videos=40, dim=96):
+    """A BigFile directory (shape.txt, id.txt, feature.bin, video2frames.txt) in the layout
+    LINAS writes (basic/bigfile.py:6-18, util/get_frameInfo.py:36-52): frame ids
+    '<video>_<frame no>' stored in SHUFFLED file order, 1..80 frames per video (some over
+    VIDEO_MAX_LEN=64), a few rows belonging to no video.  Returns (names, feats, video2frames)."""
+    import os
+    rng = np.random.default_rng(seed)
+    os.makedirs(datadir, exist_ok=True)
+    counts = rng.integers(1, 81, size=n_videos)
+    counts[0], counts[1] = 1, 80
+    frames = [f"vid{v:03d}_{k}" for v in range(n_videos) for k in range(1, int(counts[v]) + 1)]
+    frames += [f"orphan_{k}" for k in range(5)]
+    names = [frames[i] for i in rng.permutation(len(frames))]
+    feats = rng.standard_normal((len(names), dim), dtype=np.float32)
+    with open(os.path.join(datadir, "shape.txt"), "w") as f:
+        f.write("%d %d\n" % (len(names), dim))
+    with open(os.path.join(datadir, "id.txt"), "w") as f:
+        f.write(" ".join(names))
+    feats.tofile(os.path.join(datadir, "feature.bin"))
+    video2frames = {f"vid{v:03d}": [f"vid{v:03d}_{k}" for k in range(1, int(counts[v]) + 1)]
+                    for v in range(n_videos)}
+    with open(os.path.join(datadir, "video2frames.txt"), "w") as f:
+        f.write(str(video2frames))
+    return names, feats, video2frames
+
+
+BIGFILE_REQUESTS = [
+    ["vid003_2", "vid000_1", "nope", "vid003_2", "orphan_4"],   # duplicate + unknown name
+    ["vid001_%d" % k for k in range(80, 0, -3)],              # reverse order
+]
