@@ -27,6 +27,7 @@ TOPK_MAX = 2048
 MAX_CHUNKS = 16
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
+PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD = 0, 1, 2, 3, 4
 
 
 class Rows(C.Structure):
@@ -79,6 +80,8 @@ SIGNATURES = {
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_topk": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp]),
+    "cmve_pairwise": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i32, _f64, _f64, _vp,
+                                _i32, _i64]),
     "cmve_bigfile_open": (C.c_int, [C.c_char_p, _i64, _i32, _P(_vp)]),
     "cmve_bigfile_close": (C.c_int, [_vp]),
     "cmve_bigfile_gather": (C.c_int, [_vp, _vp, _i64, _vp, _i32]),

@@ -154,6 +154,22 @@ def sim_store(q: RowSet, g: RowSet, alpha: float = 1.0, beta: float = 0.0, mode:
     return out
 
 
+def pairwise(a: torch.Tensor, b: torch.Tensor, metric: int, alpha: float = 1.0, beta: float = 0.0,
+             out_dtype=torch.float64) -> torch.Tensor:
+    """out[i, j] = alpha * f(a_i, b_j) + beta for a non-cosine metric (K10, fp64 accumulation)."""
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
+        raise ValueError(f"pairwise: shapes {tuple(a.shape)} and {tuple(b.shape)} do not match")
+    # row-strided views go in as they are (lda >= D); anything else is made contiguous
+    a = a if a.stride(1) == 1 and a.stride(0) >= a.shape[1] else a.contiguous()
+    b = b if b.stride(1) == 1 and b.stride(0) >= b.shape[1] else b.contiguous()
+    out = torch.empty((a.shape[0], b.shape[0]), dtype=out_dtype, device=a.device)
+    if a.shape[0] and b.shape[0]:
+        check(lib.cmve_pairwise(handle(a.device), _ptr(a), _dtype_code(a), a.stride(0), a.shape[0], _ptr(b),
+                                _dtype_code(b), b.stride(0), b.shape[0], a.shape[1], metric, float(alpha),
+                                float(beta), _ptr(out), _dtype_code(out), out.stride(0)), "cmve_pairwise")
+    return out
+
+
 def csr(lists: Sequence[Sequence[int]], device) -> Tuple[torch.Tensor, torch.Tensor]:
     """Python GT lists -> (offsets int64 [n+1], indices int32) device tensors."""
     lens = np.fromiter((len(l) for l in lists), dtype=np.int64, count=len(lists))

@@ -2,7 +2,9 @@
 
 Same names, argument meaning and return types as the reference:
   l2norm(X)                                  evaluation.py:10-14
-  cal_error(videos, captions, measure)       evaluation.py:17-36  -> ndarray[N_c, N_v] (= -cos)
+  cal_error(videos, captions, measure)       evaluation.py:17-36  -> ndarray[N_c, N_v] (= -cos; the
+                                             euclidean / l1 / l2 / l1_norm / l2_norm / jaccard branches
+                                             on the K10 all-pairs kernel)
   cal_error_batch(..., batch_size)           evaluation.py:41-72
   cal_simi(captions, videos, measure)        evaluation.py:75-84  -> ndarray[N_c, N_v] (= +cos)
   encode_vid / encode_text                   evaluation.py:88-171
@@ -18,7 +20,7 @@ import numpy as np
 import torch
 
 from .. import engine
-from .._lib import SIM_BF16X3
+from .._lib import SIM_BF16X3, PW_L1, PW_L2, PW_JACCARD
 
 
 class ErrorMatrix(np.ndarray):
@@ -57,25 +59,55 @@ def _cosine(videos, captions, sign):
     return _as_error_matrix(out.cpu().numpy(), caps, vids, sign)
 
 
+# scipy cdist branches of evaluation.py:22-33 / 56-67: measure -> (metric, alpha(D), beta), fp64 out
+_CDIST = {
+    'euclidean': (PW_L2, lambda D: 1.0, 0.0),
+    'l2': (PW_L2, lambda D: 1.0, 0.0),
+    'l1': (PW_L1, lambda D: 1.0, 0.0),
+    'l1_norm': (PW_L1, lambda D: -1.0 / D, -1.0),
+    'l2_norm': (PW_L2, lambda D: -1.0 / D, -1.0),
+}
+
+
+def _measure(videos, captions, measure):
+    dev = engine.default_device()
+    if measure in _CDIST:  # cdist works in fp64 whatever the input dtype
+        metric, alpha, beta = _CDIST[measure]
+        c = engine.to_device(np.asarray(captions), dev, torch.float64)
+        v = engine.to_device(np.asarray(videos), dev, torch.float64)
+        return engine.pairwise(c, v, metric, alpha(v.shape[1]), beta, torch.float64).cpu().numpy()
+    if measure == 'jaccard':  # torch.Tensor(...) -> fp32 inputs, -jaccard_sim, returned as a torch tensor
+        c = engine.to_device(np.asarray(captions), dev, torch.float32)
+        v = engine.to_device(np.asarray(videos), dev, torch.float32)
+        return engine.pairwise(c, v, PW_JACCARD, -1.0, 0.0, torch.float32).cpu()
+    raise ValueError(f"cmve.cal_error: unknown measure {measure!r}")
+
+
 def cal_error(videos, captions, measure='cosine'):
-    """errors[N_c, N_v] = -cos(caption_i, video_j)  (evaluation.py:17-21)."""
+    """errors[N_c, N_v] (evaluation.py:17-36): -cos, or the cdist / jaccard branches."""
     if measure == 'cosine':
         return _cosine(videos, captions, -1)
-    raise NotImplementedError(
-        f"cmve.cal_error: measure {measure!r} is not on the MI355X hot path yet (cosine only; "
-        "euclidean/l1/l2/jaccard are SURVEY section 8f 'next' item 4)")
+    return _measure(videos, captions, measure)
 
 
 def cal_error_batch(videos, captions, measure='cosine', batch_size=2000):
-    """evaluation.py:41-72 -- the batching only matters for the jaccard branch."""
-    return cal_error(videos, captions, measure)
+    """evaluation.py:41-72 -- the caption batching only bounds the reference's jaccard memory;
+    the all-pairs kernel never materialises the [N_c, N_v, D] broadcast, so one call covers it
+    (the jaccard result is a float32 ndarray here, as np.append makes it in the reference)."""
+    out = cal_error(videos, captions, measure)
+    return out.numpy() if measure == 'jaccard' else out
 
 
 def cal_simi(captions, videos, measure='cosine'):
-    """+cos(caption_i, video_j)  (evaluation.py:75-84)."""
+    """+cos(caption_i, video_j) or +jaccard as a float32 torch tensor (evaluation.py:75-84)."""
     if measure == 'cosine':
         return _cosine(videos, captions, +1)
-    raise NotImplementedError(f"cmve.cal_simi: measure {measure!r} not supported (cosine only)")
+    if measure == 'jaccard':
+        dev = engine.default_device()
+        c = engine.to_device(np.asarray(captions), dev, torch.float32)
+        v = engine.to_device(np.asarray(videos), dev, torch.float32)
+        return engine.pairwise(c, v, PW_JACCARD, 1.0, 0.0, torch.float32).cpu()
+    raise ValueError(f"cmve.cal_simi: measure {measure!r} has no branch in the reference (evaluation.py:75-84)")
 
 
 def _encode(encoder_call, data_loader, return_ids):

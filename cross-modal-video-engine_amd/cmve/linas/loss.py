@@ -11,7 +11,7 @@ import torch
 import torch.nn as nn
 
 from .. import engine
-from .._lib import lib, check
+from .._lib import lib, check, PW_SQ_L2, PW_L1, PW_ORDER, PW_JACCARD
 
 
 def _h(t):
@@ -34,6 +34,53 @@ def gemm_f32(a: torch.Tensor, b: torch.Tensor, trans_a=False, trans_b=False, alp
 def cosine_sim(im, s):
     """loss.py:7-10: im.mm(s.t())."""
     return gemm_f32(im, s, trans_b=True)
+
+
+# ---- non-cosine similarities (loss.py:13-73) on the K10 all-pairs kernel: score[i_im, j_s] ----
+# forward only: a caller that needs their gradient gets an error, not a silently detached result
+def _pw(im, s, metric, alpha, beta):
+    if torch.is_grad_enabled() and (im.requires_grad or s.requires_grad):
+        raise NotImplementedError("cmve: the non-cosine similarities are forward-only (evaluation); their "
+                                  "backward is not on the MI355X path")
+    dev = im.device if im.is_cuda else engine.default_device()
+    a = engine.to_device(im, dev, torch.float32)
+    b = engine.to_device(s, dev, torch.float32)
+    return engine.pairwise(a, b, metric, alpha, beta, torch.float32)
+
+
+def order_sim(im, s):
+    """loss.py:13-19: -sqrt(sum max(0, s_j - im_i)^2)."""
+    return _pw(im, s, PW_ORDER, -1.0, 0.0)
+
+
+def euclidean_sim(im, s):
+    """loss.py:22-28: -sum (s_j - im_i)^2 (squared, as the reference)."""
+    return _pw(im, s, PW_SQ_L2, -1.0, 0.0)
+
+
+def L1_sim(im, s):
+    """loss.py:31-37."""
+    return _pw(im, s, PW_L1, -1.0, 0.0)
+
+
+def L1_sim_norm(im, s):
+    """loss.py:39-45: L1 / D - 1."""
+    return _pw(im, s, PW_L1, 1.0 / im.shape[1], -1.0)
+
+
+def L2_sim(im, s):
+    """loss.py:48-54: -sum (s_j - im_i)^2."""
+    return _pw(im, s, PW_SQ_L2, -1.0, 0.0)
+
+
+def L2_sim_norm(im, s):
+    """loss.py:56-62: sum (s_j - im_i)^2 / D - 1."""
+    return _pw(im, s, PW_SQ_L2, 1.0 / im.shape[1], -1.0)
+
+
+def jaccard_sim(im, s):
+    """loss.py:65-73: sum min / sum max."""
+    return _pw(im, s, PW_JACCARD, 1.0, 0.0)
 
 
 _DIRS = {"v2t": 1, "t2v": 2, "all": 3}
@@ -92,7 +139,7 @@ class TripletLoss(nn.Module):
                                 self.cost_style != 'sum')
 
 
-NAME_TO_SIM = {'cosine': cosine_sim}
+NAME_TO_SIM = {'cosine': cosine_sim, 'order': order_sim, 'euclidean': euclidean_sim, 'jaccard': jaccard_sim}
 
 
 def get_sim(name):

@@ -671,9 +671,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     n0 = n0n;
     thr_hi_v = thn_hi;
     thr_lo_v = thn_lo;
-#pragma unroll
     for (int i = 0; i < TM; ++i)
-#pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
 #undef CMVE_BAR

@@ -323,6 +323,20 @@ int cmve_gt_positions_from_matrix(cmve_handle_t h, const void* errors, int32_t d
 int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
               float* scores_ws, int32_t* out_idx, double* out_score, int32_t* overflow);
 
+/* ---- non-cosine measures ---------------------------------
+ * K10: out[i, j] = alpha * f(A_i, B_j) + beta over all pairs, fp64 accumulation.
+ *   CMVE_PW_SQ_L2   sum (a-b)^2          CMVE_PW_L2      sqrt(sum (a-b)^2)
+ *   CMVE_PW_L1      sum |a-b|            CMVE_PW_ORDER   sqrt(sum max(0, b-a)^2)
+ *   CMVE_PW_JACCARD sum min(a,b) / sum max(a,b)
+ * Replaces: LINAS-engine/evaluation.py:22-35,56-71 (scipy cdist 'euclidean' / 'minkowski' p=1,
+ * l1_norm / l2_norm = -f/D - 1, -jaccard) and LINAS-engine/loss.py:13-73 (order_sim = -ORDER,
+ * euclidean_sim / L2_sim = -SQ_L2, L1_sim = -L1, L1_sim_norm = L1/D - 1, L2_sim_norm = SQ_L2/D - 1,
+ * jaccard_sim).  A, B: f32/f64 rows (device); out f32/f64 [na, nb] (device). */
+enum cmve_pw_metric { CMVE_PW_SQ_L2 = 0, CMVE_PW_L2 = 1, CMVE_PW_L1 = 2, CMVE_PW_ORDER = 3, CMVE_PW_JACCARD = 4 };
+int cmve_pairwise(cmve_handle_t h, const void* A, int32_t a_dtype, int64_t lda, int64_t na, const void* B,
+                  int32_t b_dtype, int64_t ldb, int64_t nb, int64_t d, int32_t metric, double alpha, double beta,
+                  void* out, int32_t out_dtype, int64_t ldo);
+
 /* ---- on-disk feature store -------------------------------
  * BigFile: feature.bin = n_rows x dim float32, row-major (LINAS-engine/basic/bigfile.py:6-18).
  * These are HOST calls (they read the page cache); the device variant also enqueues H2D copies on
