@@ -82,6 +82,20 @@ SIGNATURES = {
     "cmve_topk": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp]),
     "cmve_pairwise": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i32, _f64, _f64, _vp,
                                 _i32, _i64]),
+    "cmve_bn_train_fwd": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "cmve_bn_train_bwd": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _f64, _vp, _i64, _vp, _vp]),
+    "cmve_gemm_f32_ex": (C.c_int, [_vp, _i32, _i32, _i64, _i64, _i64, _f32, _vp, _i64, _vp, _i64, _f32, _vp, _i64,
+                                   _vp, _i32]),
+    "cmve_col_sum": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
+    "cmve_resid_relu": (C.c_int, [_vp, _vp, _vp, _i64, _vp]),
+    "cmve_relu_grad": (C.c_int, [_vp, _vp, _vp, _i64, _vp]),
+    "cmve_l2norm_bwd": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _i64]),
+    "cmve_dropout": (C.c_int, [_vp, _vp, _i64, C.c_float, C.c_uint64, C.c_uint64, _vp, _vp, _vp]),
+    "cmve_mask_scale": (C.c_int, [_vp, _vp, _vp, _i64, C.c_float, _vp]),
+    "cmve_grad_norm_multi": (C.c_int, [_vp, _i32, _vp, _vp, _f64, _vp, _vp]),
+    "cmve_scale_multi": (C.c_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cmve_adam_multi": (C.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _f64, _vp,
+                                  _vp]),
     "cmve_bigfile_open": (C.c_int, [C.c_char_p, _i64, _i32, _P(_vp)]),
     "cmve_bigfile_close": (C.c_int, [_vp]),
     "cmve_bigfile_gather": (C.c_int, [_vp, _vp, _i64, _vp, _i32]),

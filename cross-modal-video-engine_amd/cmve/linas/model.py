@@ -6,7 +6,8 @@
   temporal pools                          model.py:152-166 (gru mean / masked max / max_pool1d)
 Modules keep the reference's parameter names, so reference checkpoints load with
 ``load_state_dict`` (slot layout model.py:387-404).  Inference (eval) runs on the HIP kernels;
-a module in training mode raises: the projection-head training step is SURVEY 8f 'next' item 3.
+training mode (batch-statistics BN, dropout, autograd backward) runs on the K11 functions of
+``cmve.linas.train``.
 """
 from __future__ import annotations
 
@@ -129,9 +130,9 @@ class MFC(nn.Module):
     def forward(self, inputs):
         if self.n_fc <= 1:
             return inputs
-        if self.training:
-            raise NotImplementedError("cmve MFC: training-mode forward (batch-stat BN + backward) is not on the "
-                                      "MI355X path yet; call .eval() for inference")
+        if self.training:  # batch-statistics BN, dropout, autograd backward (cmve.linas.train, K11)
+            from .train import mfc_train_forward
+            return mfc_train_forward(self, inputs)
         n_lin = min(self.n_fc, 5) - 1
         bn = bn_eval_affine(self.bn_1) if (self.have_bn and self.have_last_bn) else None
         feats = None
@@ -159,7 +160,11 @@ class Latent_mapping(nn.Module):
     def forward(self, features):
         latent = self.mapping(features)
         if self.l2norm:
-            latent = globals()["l2norm"](latent)
+            if self.training:
+                from .train import l2norm_train
+                latent = l2norm_train(latent)
+            else:
+                latent = globals()["l2norm"](latent)
         return latent
 
 

@@ -201,6 +201,19 @@ __global__ __launch_bounds__(256) void l2norm_kernel(const TI* __restrict__ x, i
   for (int64_t k = lane; k < d; k += 64) yr[k] = (TO)((double)xr[k] / den);
 }
 
+int ensure_scratch(cmve_handle* h, size_t bytes) {
+  if (h->scratch_bytes >= bytes) return CMVE_OK;
+  if (h->scratch) {
+    CMVE_HIP(hipStreamSynchronize(h->stream));
+    CMVE_HIP(hipFree(h->scratch));
+    h->scratch = nullptr;
+    h->scratch_bytes = 0;
+  }
+  const size_t grown = std::max(bytes, (size_t)1 << 20);
+  CMVE_HIP(hipMalloc(&h->scratch, grown));
+  h->scratch_bytes = grown;
+  return CMVE_OK;
+}
 }  // namespace cmve
 
 using namespace cmve;
@@ -229,8 +242,10 @@ int cmve_set_stream(cmve_handle_t h, void* hip_stream) {
   return CMVE_OK;
 }
 
+
 int cmve_destroy(cmve_handle_t h) {
   if (h) {
+    if (h->scratch) (void)hipFree(h->scratch);
     for (hipEvent_t e : h->ev)
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->tev)

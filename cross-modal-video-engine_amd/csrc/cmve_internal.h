@@ -16,12 +16,17 @@ struct cmve_handle {
   hipEvent_t ev[CMVE_MAX_CHUNKS + 2] = {};
   hipEvent_t tev[2 * CMVE_MAX_CHUNKS] = {};  // timing: around each chunk's MFMA pass
   int last_chunks = 0;
+  // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
 };
 
 namespace cmve {
 
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// make h->scratch at least `bytes` (synchronises the stream and reallocates only when it grows)
+int ensure_scratch(cmve_handle* h, size_t bytes);
 
 #define CMVE_REQUIRE(cond, ...)            \
   do {                                     \

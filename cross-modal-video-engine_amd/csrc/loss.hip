@@ -1,6 +1,6 @@
 // K6 / K7: contrastive losses over a B x B score matrix S (rows = videos im / predictions,
-// columns = captions s / targets), forward + backward, plus a tiled fp32 GEMM for the
-// gradient products dL/dim = dS . s and dL/ds = dS^T . im.
+// columns = captions s / targets), forward + backward, plus an exact-fp32 MFMA GEMM for the
+// gradient products dL/dim = dS . s and dL/ds = dS^T . im (and the training heads' GEMMs, K11).
 //
 //   K6  TripletLoss  LINAS-engine/loss.py:83-153
 //       cost_s [i,j] = [m + S_ij - S_ii]_+ (j != i), reduced over j (dim 1)   direction v2t
@@ -184,51 +184,130 @@ __global__ __launch_bounds__(256) void infonce_combine_kernel(const float* __res
 // ---------------- fp32 GEMM (gradient products) ----------------
 // C[M,N] = alpha * op(A)[M,K] . B[K,N] + beta * C ; op(A) = A (transA=0, A[M,K]) or A^T (A[K,M]).
 // 64x64 tiles, 256 threads x (4x4) outputs, K step 16 through LDS, fp32 FMA chain.
-__global__ __launch_bounds__(256) void gemm_f32_kernel(int transA, int transB, int M, int N, int K, float alpha,
-                                                       const float* __restrict__ A, int64_t lda,
-                                                       const float* __restrict__ Bm, int64_t ldb, float beta,
-                                                       float* __restrict__ C, int64_t ldc) {
-  __shared__ float As[16][64 + 1];
-  __shared__ float Bs[16][64 + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    for (int e = threadIdx.x; e < 16 * 64; e += 256) {
-      const int kk = e / 64, mm = e % 64;
-      const int gm = m0 + mm, gk = k0 + kk;
-      float av = 0.f;
-      if (gm < M && gk < K) av = transA ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
-      As[kk][mm] = av;
-      const int gn = n0 + mm;
-      Bs[kk][mm] = (gn < N && gk < K) ? (transB ? Bm[(int64_t)gn * ldb + gk] : Bm[(int64_t)gk * ldb + gn]) : 0.f;
+// C = alpha * op(A) . op(B) + beta * C (+ bias[n]) (relu), on v_mfma_f32_16x16x4_f32: each
+// K-slice is bit-for-bit a k-ordered fp32 fmaf chain (cdna_hip_programming.md, FP32-input MFMA).
+// 64 x 64 block tile, 4 waves of 32 x 32 (2 x 2 MFMA tiles = 4 independent accumulators), K staged
+// through LDS 32 at a time as [k][m] / [k][n] (+4 pad); global loads coalesced along whichever
+// dimension is contiguous (float4 when every operand allows it).
+// Split-K: small M x N grids (the B x B score GEMMs, B x 1024 projections) cannot fill 256 CUs with
+// one serial K loop per tile, so blockIdx.z takes a K-slice and writes raw partials to scratch;
+// gemm_splitk_reduce_kernel sums the slices in fixed z order (deterministic) and applies the epilogue.
+typedef float gf32x4 __attribute__((ext_vector_type(4)));
+constexpr int GT = 64, GK = 32, GP = GT + 4;
+
+template <bool VEC>
+__device__ __forceinline__ void gemm_stage(const float* __restrict__ X, int64_t ldx, bool kmajor, int r0, int R,
+                                           int k0, int K, float (*S)[GP]) {
+  // stage op(X)[r0 .. r0+64)[k0 .. k0+32) into S[k][r]; kmajor: X[k][r] (r contiguous), else X[r][k]
+  const int tid = threadIdx.x;
+  if constexpr (VEC) {
+#pragma unroll
+    for (int e = 0; e < GT * GK / 1024; ++e) {
+      const int idx = e * 256 + tid;  // float4 index
+      if (kmajor) {
+        const int kk = idx / (GT / 4), rr = (idx % (GT / 4)) * 4;
+        const int gk = k0 + kk, gr = r0 + rr;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < K && gr < R) v = *reinterpret_cast<const float4*>(X + (int64_t)gk * ldx + gr);
+        S[kk][rr] = v.x; S[kk][rr + 1] = v.y; S[kk][rr + 2] = v.z; S[kk][rr + 3] = v.w;
+      } else {
+        const int rr = idx / (GK / 4), kk = (idx % (GK / 4)) * 4;
+        const int gk = k0 + kk, gr = r0 + rr;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < K && gr < R) v = *reinterpret_cast<const float4*>(X + (int64_t)gr * ldx + gk);
+        S[kk][rr] = v.x; S[kk + 1][rr] = v.y; S[kk + 2][rr] = v.z; S[kk + 3][rr] = v.w;
+      }
     }
+  } else {
+#pragma unroll
+    for (int e = 0; e < GT * GK / 256; ++e) {
+      const int idx = e * 256 + tid;
+      int rr, kk;
+      if (kmajor) { kk = idx / GT; rr = idx % GT; } else { rr = idx / GK; kk = idx % GK; }
+      const int gr = r0 + rr, gk = k0 + kk;
+      float v = 0.f;
+      if (gr < R && gk < K) v = kmajor ? X[(int64_t)gk * ldx + gr] : X[(int64_t)gr * ldx + gk];
+      S[kk][rr] = v;
+    }
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(int transA, int transB, int M, int N, int K, int kslice,
+                                                       float alpha, const float* __restrict__ A, int64_t lda,
+                                                       const float* __restrict__ Bm, int64_t ldb, float beta,
+                                                       float* __restrict__ C, int64_t ldc,
+                                                       const float* __restrict__ bias, int relu,
+                                                       float* __restrict__ part) {
+  __shared__ float As[GK][GP];
+  __shared__ float Bs[GK][GP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int kb = blockIdx.z * kslice, ke = min(K, kb + kslice);
+  gf32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = gf32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += GK) {
+    gemm_stage<VEC>(A, lda, transA != 0, m0, M, k0, ke, As);    // op(A)[m][k]
+    gemm_stage<VEC>(Bm, ldb, transB == 0, n0, N, k0, ke, Bs);   // op(B)[k][n]: B[k][n] is n-contiguous
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      float a[4], b[4];
+    for (int ks = 0; ks < GK; ks += 4) {
+      const int kr = ks + (lane >> 4);
+      float a[2], b[2];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] = As[kk][ty * 4 + u];
-        b[u] = Bs[kk][tx * 4 + u];
+      for (int i = 0; i < 2; ++i) {
+        a[i] = As[kr][wm + i * 16 + (lane & 15)];
+        b[i] = Bs[kr][wn + i * 16 + (lane & 15)];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = fmaf(a[u], b[v], acc[u][v]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
+  // C/D map of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int gm = m0 + ty * 4 + u, gn = n0 + tx * 4 + v;
-      if (gm < M && gn < N) {
-        float* c = C + (int64_t)gm * ldc + gn;
-        *c = alpha * acc[u][v] + (beta != 0.f ? beta * *c : 0.f);
+    for (int j = 0; j < 2; ++j) {
+      const int gn = n0 + wn + j * 16 + (lane & 15);
+      if (gn >= N) continue;
+      const float bn = (bias && !part) ? bias[gn] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (gm >= M) continue;
+        if (part) {
+          part[((int64_t)blockIdx.z * M + gm) * N + gn] = acc[i][j][r];
+        } else {
+          float* c = C + (int64_t)gm * ldc + gn;
+          float v = alpha * acc[i][j][r] + (beta != 0.f ? beta * *c : 0.f) + bn;
+          if (relu) v = v > 0.f ? v : 0.f;
+          *c = v;
+        }
       }
     }
+}
+
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __restrict__ part, int splits, int M,
+                                                                 int N, float alpha, float beta,
+                                                                 float* __restrict__ C, int64_t ldc,
+                                                                 const float* __restrict__ bias, int relu) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    float s = part[i];
+    for (int z = 1; z < splits; ++z) s += part[(int64_t)z * total + i];
+    const int gm = (int)(i / N), gn = (int)(i % N);
+    float* c = C + (int64_t)gm * ldc + gn;
+    float v = alpha * s + (beta != 0.f ? beta * *c : 0.f) + (bias ? bias[gn] : 0.f);
+    if (relu) v = v > 0.f ? v : 0.f;
+    *c = v;
+  }
 }
 
 }  // namespace cmve
@@ -292,15 +371,51 @@ extern "C" int cmve_infonce_bwd(cmve_handle_t h, const float* S, int64_t ld, int
   return check_launch("infonce_bwd");
 }
 
+static int gemm_f32_launch(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K,
+                           float alpha, const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                           int64_t ldc, const float* bias, int32_t relu, const char* who) {
+  CMVE_REQUIRE(h && A && B && C, "%s: NULL argument", who);
+  CMVE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "%s: bad shape", who);
+  CMVE_REQUIRE(ldc >= N && lda >= (transA ? M : K) && ldb >= (transB ? K : N), "%s: leading dimension too small", who);
+  if (M == 0 || N == 0) return CMVE_OK;
+  CMVE_REQUIRE((M + GT - 1) / GT < 65536, "%s: M too large for the grid", who);
+  const int64_t nbm = (M + GT - 1) / GT, nbn = (N + GT - 1) / GT, blocks = nbm * nbn;
+  // split K until the grid reaches ~2 blocks per CU, keeping >= 2 K-tiles per slice
+  int64_t splits = 1;
+  while (blocks * splits * 2 <= 512 && K / (splits * 2) >= 2 * GK) splits *= 2;
+  const int64_t kslice = ((K + splits * GK - 1) / (splits * GK)) * GK;
+  splits = std::max<int64_t>(1, (K + kslice - 1) / kslice);
+  float* part = nullptr;
+  if (splits > 1) {
+    const int rc = ensure_scratch(h, (size_t)splits * M * N * sizeof(float));
+    if (rc != CMVE_OK) return rc;
+    part = (float*)h->scratch;
+  }
+  // float4 staging needs 16-B aligned rows and 4-multiples along every contiguous extent
+  auto al = [](const void* p, int64_t ld) { return ((uintptr_t)p % 16 == 0) && (ld % 4 == 0); };
+  const bool vec = al(A, lda) && al(B, ldb) && (transA ? M % 4 == 0 : K % 4 == 0) && (transB ? K % 4 == 0 : N % 4 == 0);
+  dim3 grid((unsigned)nbn, (unsigned)nbm, (unsigned)splits);
+  if (vec)
+    hipLaunchKernelGGL(gemm_f32_kernel<true>, grid, dim3(256), 0, h->stream, transA, transB, (int)M, (int)N, (int)K,
+                       (int)kslice, alpha, A, lda, B, ldb, beta, C, ldc, bias, relu, part);
+  else
+    hipLaunchKernelGGL(gemm_f32_kernel<false>, grid, dim3(256), 0, h->stream, transA, transB, (int)M, (int)N, (int)K,
+                       (int)kslice, alpha, A, lda, B, ldb, beta, C, ldc, bias, relu, part);
+  if (splits > 1)
+    hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)std::min<int64_t>((M * N + 255) / 256, 2048)),
+                       dim3(256), 0, h->stream, part, (int)splits, (int)M, (int)N, alpha, beta, C, ldc, bias, relu);
+  return check_launch(who);
+}
+
 extern "C" int cmve_gemm_f32(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K, float alpha,
                              const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                              int64_t ldc) {
-  CMVE_REQUIRE(h && A && B && C, "cmve_gemm_f32: NULL argument");
-  CMVE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30),
-               "cmve_gemm_f32: bad shape");
-  if (M == 0 || N == 0) return CMVE_OK;
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64));
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, h->stream, transA, transB, (int)M, (int)N, (int)K, alpha, A, lda, B,
-                     ldb, beta, C, ldc);
-  return check_launch("gemm_f32");
+  return gemm_f32_launch(h, transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr, 0, "cmve_gemm_f32");
+}
+
+extern "C" int cmve_gemm_f32_ex(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K,
+                                float alpha, const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
+                                float* C, int64_t ldc, const float* bias, int32_t relu) {
+  return gemm_f32_launch(h, transA, transB, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, relu,
+                         "cmve_gemm_f32_ex");
 }

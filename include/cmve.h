@@ -203,11 +203,15 @@ int cmve_infonce_fwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, flo
 int cmve_infonce_bwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float scale, int32_t dir,
                      const float* g, const double* row_lse, const double* col_lse, float* dS, int64_t ldd);
 
-/* fp32 GEMM for the loss gradient products: C = alpha * op(A) . op(B) + beta * C
- * (op = transpose when trans* != 0; row-major; fp32 FMA chain). */
+/* fp32 GEMM for the loss gradient products and the training heads: C = alpha * op(A) . op(B) + beta * C
+ * (op = transpose when trans* != 0; row-major) on v_mfma_f32_16x16x4_f32 -- each output is exactly a
+ * k-ordered fp32 fmaf chain.  _ex adds bias[N] (nullable) and relu after the beta term. */
 int cmve_gemm_f32(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K,
                   float alpha, const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
                   float* C, int64_t ldc);
+int cmve_gemm_f32_ex(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M, int64_t N, int64_t K,
+                     float alpha, const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
+                     float* C, int64_t ldc, const float* bias, int32_t relu);
 
 /*
  * K5a -- exact fp64 GT scores and rank thresholds for one direction.
@@ -336,6 +340,51 @@ enum cmve_pw_metric { CMVE_PW_SQ_L2 = 0, CMVE_PW_L2 = 1, CMVE_PW_L1 = 2, CMVE_PW
 int cmve_pairwise(cmve_handle_t h, const void* A, int32_t a_dtype, int64_t lda, int64_t na, const void* B,
                   int32_t b_dtype, int64_t ldb, int64_t nb, int64_t d, int32_t metric, double alpha, double beta,
                   void* out, int32_t out_dtype, int64_t ldo);
+
+/* ---- training step of the projection heads ---------------
+ * K11: what LINAS-engine/model.py:984-1004 (train_emb, style 'GT') runs around the GEMMs (K3 forward,
+ * cmve_gemm_f32 backward) and the losses (K6/K7).  Device pointers, fp32 rows; statistics in fp64.
+ *   cmve_bn_train_fwd  BatchNorm1d training forward (model.py:83-85,111-112): batch mean / biased
+ *                      variance normalise; running_mean/var (nullable) updated with momentum and the
+ *                      unbiased variance; save_mean / save_invstd [d] kept for the backward.  n > 1.
+ *   cmve_bn_train_bwd  dx, dgamma, dbeta (each nullable) from dy and x (batch statistics recomputed in fp64).
+ *   cmve_col_sum       out[d] = column sums of x [n, d] (nn.Linear bias gradient).
+ *   cmve_resid_relu    out = resid + relu(z)  (model.py:104-109); cmve_relu_grad: dz = dout * (z > 0).
+ *   cmve_l2norm_bwd    gradient of y = x / ||x|| (model.py:35-40, no epsilon).
+ *   cmve_dropout       y = keep ? x / (1 - p) : 0, keep = hash(seed, offset + i) >= p (splitmix64
+ *                      finaliser; nn.Dropout semantics, NOT torch's random stream); mask (nullable)
+ *                      = keep bytes; call_counter (device int64, nullable): offset += counter << 32, then
+ *                      counter += 1 on the stream (graph-capturable); cmve_mask_scale applies a mask (the backward).
+ * Multi-tensor calls take HOST arrays of n device pointers / sizes (launched 24 tensors at a time,
+ * pointers passed by value); all arithmetic stays on the device (no host synchronisation):
+ *   cmve_grad_norm_multi  total = ||all grads||_2 (fp64 sums, fixed order) and
+ *                         coef = min(1, max_norm / (total + 1e-6)) (torch clip_grad_norm_, model.py:1000-1001);
+ *                         coef / total_norm are device f32[1] (either nullable).
+ *   cmve_scale_multi      x_i *= coef[0] (the clip itself).
+ *   cmve_adam_multi       one torch.optim.Adam update per tensor (model.py:593; amsgrad off), steps[i] >= 1
+ *                         (the tensor's step count after this update); grad_scale (device f32[1], nullable):
+ *                         the clip coefficient, applied to and written back into the grads first;
+ *                         dev_step (device int64, nullable): capturable mode -- incremented on the stream and
+ *                         used as every tensor's step (steps may then be NULL). */
+int cmve_bn_train_fwd(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, const float* gamma,
+                      const float* beta, double eps, double momentum, float* running_mean, float* running_var,
+                      float* y, int64_t ldy, float* save_mean, float* save_invstd);
+int cmve_bn_train_bwd(cmve_handle_t h, const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t n,
+                      int64_t d, const float* gamma, double eps, float* dx, int64_t lddx, float* dgamma, float* dbeta);
+int cmve_col_sum(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, float* out);
+int cmve_resid_relu(cmve_handle_t h, const float* z, const float* resid, int64_t n, float* out);
+int cmve_relu_grad(cmve_handle_t h, const float* z, const float* dout, int64_t n, float* dz);
+int cmve_l2norm_bwd(cmve_handle_t h, const float* x, int64_t ldx, const float* dy, int64_t lddy, int64_t n, int64_t d,
+                    float* dx, int64_t lddx);
+int cmve_dropout(cmve_handle_t h, const float* x, int64_t n, float p, uint64_t seed, uint64_t offset, float* y,
+                 uint8_t* mask, int64_t* call_counter);
+int cmve_mask_scale(cmve_handle_t h, const float* x, const uint8_t* mask, int64_t n, float scale, float* y);
+int cmve_grad_norm_multi(cmve_handle_t h, int32_t n, float* const* grads, const int64_t* numels, double max_norm,
+                         float* coef, float* total_norm);
+int cmve_scale_multi(cmve_handle_t h, int32_t n, float* const* xs, const int64_t* numels, const float* coef);
+int cmve_adam_multi(cmve_handle_t h, int32_t n, float* const* params, float* const* grads, float* const* exp_avgs,
+                    float* const* exp_avg_sqs, const int64_t* numels, const int64_t* steps, double lr, double beta1,
+                    double beta2, double eps, double weight_decay, const float* grad_scale, int64_t* dev_step);
 
 /* ---- on-disk feature store -------------------------------
  * BigFile: feature.bin = n_rows x dim float32, row-major (LINAS-engine/basic/bigfile.py:6-18).
