@@ -93,22 +93,40 @@ __global__ __launch_bounds__(256) void triplet_grad_kernel(const float* __restri
       if (act && margin + sij - S[(int64_t)j * ld + j] >= 0.f) v += gr;
     }
   } else {
-    // d/dS_ii of -S_ii in every active row-i term and every active column-i term
+    // d/dS_ii of -S_ii in every active row-i / column-i term.  max_violation: only the argmax term of
+    // row i and of column i can be active (O(1)); sum style: triplet_diag_sum_kernel writes the diagonal.
+    if (!max_violation) return;
     float cnt = 0.f;
-    for (int k = 0; k < B; ++k) {
-      if (k == i) continue;
-      if (dir & 1) {
-        const bool act = max_violation ? (rarg[i] == k) : true;
-        if (act && margin + S[(int64_t)i * ld + k] - sij >= 0.f) cnt += 1.f;
-      }
-      if (dir & 2) {
-        const bool act = max_violation ? (carg[i] == k) : true;
-        if (act && margin + S[(int64_t)k * ld + i] - sij >= 0.f) cnt += 1.f;
-      }
+    if (dir & 1) {
+      const int k = rarg[i];
+      if (k != i && margin + S[(int64_t)i * ld + k] - sij >= 0.f) cnt += 1.f;
+    }
+    if (dir & 2) {
+      const int k = carg[i];
+      if (k != i && margin + S[(int64_t)k * ld + i] - sij >= 0.f) cnt += 1.f;
     }
     v -= gr * cnt;
   }
   dS[(int64_t)i * ldd + j] = v;
+}
+
+// sum style: dS_ii = -g * (#active costs in row i + #active costs in column i), one wave per i
+__global__ __launch_bounds__(256) void triplet_diag_sum_kernel(const float* __restrict__ S, int64_t ld, int B,
+                                                               float margin, int dir, float wscale,
+                                                               const float* __restrict__ g, float* __restrict__ dS,
+                                                               int64_t ldd) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= B) return;
+  const float sii = S[(int64_t)i * ld + i];
+  int cnt = 0;
+  for (int k = lane; k < B; k += 64) {
+    if (k == i) continue;
+    if ((dir & 1) && margin + S[(int64_t)i * ld + k] - sii >= 0.f) ++cnt;
+    if ((dir & 2) && margin + S[(int64_t)k * ld + i] - sii >= 0.f) ++cnt;
+  }
+  cnt = wave_sum_i(cnt);
+  if (lane == 0) dS[(int64_t)i * ldd + i] = -(g[0] * wscale) * (float)cnt;
 }
 
 // ---------------- InfoNCE ----------------
@@ -345,6 +363,9 @@ extern "C" int cmve_triplet_bwd(cmve_handle_t h, const float* S, int64_t ld, int
   const int64_t n = (int64_t)B * B;
   hipLaunchKernelGGL(triplet_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, S, ld, B,
                      margin, max_violation, dir, wscale, g, row_arg, col_arg, dS, ldd);
+  if (!max_violation)
+    hipLaunchKernelGGL(triplet_diag_sum_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, h->stream, S, ld, B, margin,
+                       dir, wscale, g, dS, ldd);
   return check_launch("triplet_bwd");
 }
 

@@ -55,40 +55,55 @@ __global__ __launch_bounds__(256) void collate_kernel(const float* __restrict__ 
     if (f0 + e < F) origin[b * F + f0 + e] = T > 0 ? acc[e] / (float)T : NAN;
 }
 
+// block = (256-float chunk of F, video b); 4 waves split the frames (t = w, w + 4, ...), each lane owns
+// 4 consecutive features (float4); the 4 wave partials are combined through LDS in fixed wave order.
 template <int MODE>
 __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ x, int64_t sb, int64_t st, int64_t T,
                                                    int64_t F, const int32_t* __restrict__ lengths,
                                                    float* __restrict__ out, int64_t ldo) {
+  __shared__ float red[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = blockIdx.y;
-  const int64_t f0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (f0 >= F) return;
+  const int64_t f0 = (int64_t)blockIdx.x * 256 + lane * 4;
   const int64_t len = lengths ? (int64_t)lengths[b] : T;
   const int64_t tend = (MODE == 0) ? (len < T ? len : T) : T;  // MEAN_VALID stops at len
   const bool vec = (f0 + 4 <= F) && ((st & 3) == 0) && ((sb & 3) == 0) && ((F & 3) == 0);
   float acc[4];
   for (int e = 0; e < 4; ++e) acc[e] = (MODE >= 2) ? -INFINITY : 0.f;
-  for (int64_t t = 0; t < tend; ++t) {
-    const float* src = x + b * sb + t * st + f0;
-    float v[4];
-    if (vec) {
-      const f32x4_t q = *(const f32x4_t*)src;
-      v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
-    } else {
-      for (int e = 0; e < 4; ++e) v[e] = (f0 + e < F) ? src[e] : 0.f;
-    }
-    if (MODE == 2) {  // masked steps contribute x * 0
-      const float m = t < len ? 1.f : 0.f;
-      for (int e = 0; e < 4; ++e) v[e] *= m;
-    }
+  if (f0 < F) {
+#pragma unroll 4
+    for (int64_t t = w; t < tend; t += 4) {
+      const float* src = x + b * sb + t * st + f0;
+      float v[4];
+      if (vec) {
+        const f32x4_t q = *(const f32x4_t*)src;
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+      } else {
+        for (int e = 0; e < 4; ++e) v[e] = (f0 + e < F) ? src[e] : 0.f;
+      }
+      if (MODE == 2) {  // masked steps contribute x * 0
+        const float m = t < len ? 1.f : 0.f;
+        for (int e = 0; e < 4; ++e) v[e] *= m;
+      }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (MODE <= 1) acc[e] += v[e];
-      else acc[e] = (v[e] > acc[e] || v[e] != v[e]) ? v[e] : acc[e];  // torch.max propagates NaN
+      for (int e = 0; e < 4; ++e) {
+        if (MODE <= 1) acc[e] += v[e];
+        else acc[e] = (v[e] > acc[e] || v[e] != v[e]) ? v[e] : acc[e];  // torch.max propagates NaN
+      }
     }
   }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[w][lane * 4 + e] = acc[e];
+  __syncthreads();
+  if (w != 0 || f0 >= F) return;
   for (int e = 0; e < 4; ++e) {
     if (f0 + e >= F) break;
-    float r = acc[e];
+    float r = red[0][lane * 4 + e];
+    for (int k = 1; k < 4; ++k) {
+      const float q = red[k][lane * 4 + e];
+      if (MODE <= 1) r += q;
+      else r = (q > r || q != q) ? q : r;
+    }
     if (MODE == 0) r = tend > 0 ? r / (float)tend : NAN;
     if (MODE == 1) r = r / (float)T;
     out[b * ldo + f0 + e] = r;
@@ -120,7 +135,7 @@ extern "C" int cmve_temporal_pool(cmve_handle_t h, const float* x, int64_t strid
   CMVE_REQUIRE(mode >= 0 && mode <= 3, "cmve_temporal_pool: unknown mode %d", mode);
   CMVE_REQUIRE(!(mode == 0 || mode == 2) || lengths, "cmve_temporal_pool: this mode needs lengths");
   if (B == 0) return CMVE_OK;
-  dim3 grid((unsigned)((F + 1023) / 1024), (unsigned)B);
+  dim3 grid((unsigned)((F + 255) / 256), (unsigned)B);
 #define POOL(M) \
   hipLaunchKernelGGL(pool_kernel<M>, grid, dim3(256), 0, h->stream, x, stride_b, stride_t, T, F, lengths, out, ldo)
   switch (mode) {

@@ -16,7 +16,7 @@
 
 namespace cmve {
 
-constexpr int COLS = 32, RGRP = 8;  // column kernels: 32 columns x 8 row groups per 256-thread block
+constexpr int COLS = 16, RGRP = 16;  // column kernels: 16 columns x 16 row groups per 256-thread block
 
 // block-wide sum over the 4 row groups of one column; all threads get the total
 __device__ __forceinline__ double col_group_sum(double v, double (*red)[COLS]) {

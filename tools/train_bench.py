@@ -127,10 +127,13 @@ def main():
     dev = torch.device("cuda", 0)
     batches = data(dev, 4)
     res = {}
+    legs = os.environ.get("LEGS", "cmve,cmve_graph,torch_eager").split(",")
+    nan = (float("nan"), float("nan"))
     for loss_name in ("triplet", "infonce"):
-        ms_c, l_c = time_leg(cmve_step_fn(dev, loss_name), batches, warmup, steps, dev)
-        ms_g, l_g = time_leg(cmve_step_fn(dev, loss_name, graph=True), batches, warmup, steps, dev)
-        ms_t, l_t = time_leg(torch_step_fn(dev, loss_name), batches, warmup, steps, dev)
+        ms_c, l_c = time_leg(cmve_step_fn(dev, loss_name), batches, warmup, steps, dev) if "cmve" in legs else nan
+        ms_g, l_g = (time_leg(cmve_step_fn(dev, loss_name, graph=True), batches, warmup, steps, dev)
+                     if "cmve_graph" in legs else nan)
+        ms_t, l_t = time_leg(torch_step_fn(dev, loss_name), batches, warmup, steps, dev) if "torch_eager" in legs else nan
         res[loss_name] = {"cmve_ms_per_step": ms_c, "cmve_graph_ms_per_step": ms_g, "torch_eager_ms_per_step": ms_t,
                           "cmve_graph_samples_per_s": B / ms_g * 1e3, "speedup_vs_torch_eager": ms_t / ms_g,
                           "last_loss": {"cmve": l_c, "cmve_graph": l_g, "torch_eager": l_t}}
