@@ -15,8 +15,10 @@ CLI (same flags as inference.py:37-44, plus the inputs the frozen encoder would 
 ``--gallery`` is an .npz with ``video_embs`` [N, D] and ``video_ids`` (the content of the
 reference's ``video_data.pt`` cache, inference.py:57-67); ``--query-emb`` is the caption
 embedding that ``model.embed_txt_distill(process_cap(input))`` produces (inference.py:76-77).
-The frozen biGRU text encoder needs the unshipped checkpoint
-``student_support_set_8/model_best.pth.tar`` (LINAS-engine/readme.md:17), so it is an input here.
+With ``--checkpoint`` (the reference's model_best.pth.tar, loaded weights-only) and the two
+vocabularies, ``--input`` is encoded exactly as inference.py:69-77 does (cmve.linas.text.process_cap
+-> cmve.linas.checkpoint.QueryEncoder); the reference's own checkpoint
+``student_support_set_8/model_best.pth.tar`` is not shipped (LINAS-engine/readme.md:17).
 """
 from __future__ import annotations
 
@@ -63,18 +65,30 @@ def parse_args(argv=None):
                    help='npz with video_embs [N,D] and video_ids (the video_data.pt cache content)')
     p.add_argument('--query-emb', default=None, type=str,
                    help='.npy caption embedding [1,D] (output of the frozen text encoder for --input)')
+    p.add_argument('--checkpoint', default=None, type=str,
+                   help='LINAS model_best.pth.tar: encode --input with its text encoder + mapping '
+                        '(loaded weights-only, cmve.linas.checkpoint)')
+    p.add_argument('--rnn-vocab', default=None, type=str, help='rnn vocabulary (.json or the reference .pkl)')
+    p.add_argument('--bow-vocab', default=None, type=str, help='bow vocabulary (.json or the reference .pkl)')
     return p.parse_args(argv)
 
 
 def main(argv=None):
     opt = parse_args(argv)
     os.environ.setdefault("HIP_VISIBLE_DEVICES", opt.gpu)
-    if opt.query_emb is None:
-        sys.exit("cmve inference: --query-emb is required (the frozen biGRU text encoder needs the unshipped "
-                 "student_support_set_8/model_best.pth.tar checkpoint)")
+    if opt.query_emb is None and not (opt.checkpoint and opt.rnn_vocab and opt.bow_vocab):
+        sys.exit("cmve inference: give --query-emb, or --checkpoint with --rnn-vocab and --bow-vocab "
+                 "(inference.py:49-77: checkpoint + vocabularies -> process_cap -> embed_txt_distill)")
     data = np.load(opt.gallery, allow_pickle=False)
     scorer = GalleryScorer(data['video_embs'], [str(v) for v in data['video_ids']])
-    cap_emb = np.load(opt.query_emb, allow_pickle=False).astype(np.float32)
+    if opt.query_emb is not None:
+        cap_emb = np.load(opt.query_emb, allow_pickle=False).astype(np.float32)
+    else:
+        from .checkpoint import QueryEncoder
+        from . import text as T
+        enc = QueryEncoder.from_checkpoint(opt.checkpoint)
+        vocab, bow_vocab = T.load_vocab(opt.rnn_vocab), T.load_vocab(opt.bow_vocab)
+        cap_emb = enc(T.process_cap(opt.input, vocab, T.get_text_encoder('bow')(bow_vocab))).cpu().numpy()
     print(scorer.topk_ids(cap_emb, opt.topK))
 
 

@@ -497,6 +497,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         }
       }
       CMVE_STAMP(6);
+#ifdef CMVE_DBG_NOFLUSH  // diagnostic build only: no global flush of candidates / counts (results garbage)
+      if (tid == 0) *lds_ncand = 0u;
+      for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
+      return;
+#endif
       CMVE_BAR_LDS();
       // flush the block's undecided pairs with ONE global atomic
       const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
