@@ -101,6 +101,15 @@ __device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chu
   return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
 }
 
+// LDS atomic add in inline asm: the compiler drains vmcnt before any LDS write it emits while
+// LDS-DMA loads are in flight (it cannot tell the staging buffers from the epilogue scratch), which
+// made the first row count of every epilogue wait for the next tile's prefetch.  The callers
+// order these adds with CMVE_BAR_LDS (lgkmcnt(0) + s_barrier) before anything reads the counters.
+__device__ __forceinline__ void lds_add_u32_async(int* p, int v) {
+  const uint32_t addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)p;
+  asm volatile("ds_add_u32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
 // sum over the 16 lanes of each DPP row (quad xor 1, xor 2, half-row mirror, row mirror): 4 VALU
 __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
@@ -181,6 +190,28 @@ constexpr size_t stage_bytes() {
 // for the next tile stay in flight across the epilogue's barriers.
 #define CMVE_BAR_LDS() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+// Epilogue scratch as its own (static) LDS object: the staging buffers are the dynamic object that
+// the LDS-DMA loads write, and the compiler orders an LDS access after in-flight LDS-DMA (vmcnt(0))
+// only when it may alias that object -- with one shared dynamic object, the first epilogue LDS op
+// drained the next tile's prefetch.
+template <int BM, int BN, bool RANK>
+struct EpiLds {
+  int rc[BM];
+  int cc[BN];
+  unsigned long long cand[CAND_LDS];
+  unsigned ncand[2];
+  unsigned long long cand_base;
+  float thr[2 * (BM + BN)];  // [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
+};
+template <int BM, int BN>
+struct EpiLds<BM, BN, false> {
+  int rc[1], cc[1];
+  unsigned long long cand[1];
+  unsigned ncand[2];
+  unsigned long long cand_base;
+  float thr[1];
+};
+
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   using G = Geo<WM, WN, TM>;
@@ -212,14 +243,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
                                          (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
 
-  // epilogue scratch after the staging buffers (one dynamic LDS object only)
-  int* lds_rc = (int*)(smem + 2 * STAGE_BYTES);
-  int* lds_cc = lds_rc + BM;
-  unsigned long long* lds_cand = (unsigned long long*)(lds_cc + BN);
-  unsigned* lds_ncand = (unsigned*)(lds_cand + CAND_LDS);
-  unsigned long long* lds_cand_base = (unsigned long long*)(lds_ncand + 2);
-  // rank thresholds of the tile: [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
-  float* lds_thr = (float*)(lds_cand_base + 1);
+  __shared__ EpiLds<BM, BN, EPI == EPI_RANK> epi;
+  int* lds_rc = epi.rc;
+  int* lds_cc = epi.cc;
+  unsigned long long* lds_cand = epi.cand;
+  unsigned* lds_ncand = epi.ncand;
+  unsigned long long* lds_cand_base = &epi.cand_base;
+  float* lds_thr = epi.thr;
   float thr_hi_v = __builtin_nanf(""), thr_lo_v = __builtin_nanf("");
   // a tile's thresholds are fetched when its loads are issued and published to LDS in its
   // epilogue: the epilogue must not wait on HBM (8 dependent loads per wave there cost ~28%)
@@ -376,7 +406,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const uint32_t c = (rc_pack >> (8 * r)) & 0xffu;
-            if (c) atomicAdd(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
+            if (c) lds_add_u32_async(&lds_rc[wr * (TM * 16) + i * 16 + (lane >> 4) * 4 + r], (int)c);
           }
         }
       };
@@ -754,10 +784,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN>() +
-                     (EPI == EPI_RANK ? (G::BM + G::BN) * sizeof(int) + CAND_LDS * sizeof(unsigned long long) + 16 +
-                                            2 * (G::BM + G::BN) * sizeof(float)
-                                      : 0);
+  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN>();  // + the static epilogue scratch (EpiLds)
   static bool attr_done = false;
   if (!attr_done) {
     CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
