@@ -205,6 +205,34 @@ def test_ragged_shapes_and_empty_gts(torch_cuda, nq, ng, d):
         np.testing.assert_allclose(sc[i], s[i, order], rtol=0, atol=1e-13)
 
 
+def test_exact_ties_rank_bounds(torch_cuda):
+    """Collisions: gallery rows that are exact copies of a query's GT video tie with it in fp64.
+    The fused rank counts strictly better items (1 + #{s > s_gt}); the reference's rank -- the
+    first GT position in np.argsort (quicksort, not stable) -- lies in [ours, ours + #ties].
+    Top-k breaks ties by index (a stable argsort of -s)."""
+    from cmve import engine
+    rng = np.random.default_rng(11)
+    ng, nq, d = 700, 90, 96
+    gal = rng.standard_normal((ng, d))
+    gts = rng.integers(0, 300, nq)
+    dup_src = gts[:30]
+    gal[300 + np.arange(30)] = gal[dup_src]          # 30 exact duplicates of GT videos
+    gal[400 + np.arange(30)] = 2.0 * gal[dup_src]    # and 30 scaled copies (same direction)
+    qs = gal[gts] + 0.3 * rng.standard_normal((nq, d))
+    s = R.exact_scores64(qs, gal)
+    q = engine.RowSet(qs, with_lo=False)
+    g = engine.RowSet(gal, with_lo=False)
+    r, _, _ = engine.gt_rank_counts(q, g, row_gts=[[int(x)] for x in gts])
+    ref = np.array([1 + int(np.where(np.argsort(-s[i]) == gts[i])[0][0]) for i in range(nq)])
+    ties = np.array([int(np.sum(s[i] == s[i, gts[i]])) - 1 for i in range(nq)])
+    assert np.array_equal(r, R.rank_counts(s, [[int(x)] for x in gts]))
+    assert np.all(ref >= r) and np.all(ref <= r + ties)
+    assert ties[:30].min() >= 1  # the collisions are real fp64 ties
+    idx, _ = engine.topk(q, g, 8)
+    for i in range(nq):
+        assert list(idx[i]) == list(np.argsort(-s[i], kind="stable")[:8])
+
+
 def test_candidate_overflow_retry(torch_cuda):
     from cmve import engine
     v, c, vid, cid = _c1()
