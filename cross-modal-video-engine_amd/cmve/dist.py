@@ -59,6 +59,24 @@ def reduce_counts(cnt: torch.Tensor, world: int) -> torch.Tensor:
     return cnt
 
 
+def gather_rows_async(x_local: torch.Tensor, out: torch.Tensor, world: int):
+    """all_gather_into_tensor(out, x_local) as an async collective (RCCL runs it on its own stream):
+    returns the Work to .wait() on before reading `out`, or None at world 1 (plain copy)."""
+    if world == 1:
+        out.copy_(x_local)
+        return None
+    return dist.all_gather_into_tensor(out, x_local.contiguous(), async_op=True)
+
+
+def any_flag(flag: torch.Tensor, world: int) -> torch.Tensor:
+    """OR of a per-rank boolean over the ranks (all-reduce MAX), so that all ranks take the same branch."""
+    if world == 1:
+        return flag
+    o = flag.to(torch.int32).reshape(1)
+    dist.all_reduce(o, op=dist.ReduceOp.MAX)
+    return o[0] > 0
+
+
 def ranks_from(cnt: torch.Tensor, sgt: torch.Tensor, n_q: int, n_global: int) -> torch.Tensor:
     no_gt = torch.isnan(sgt[:n_q])
     c = cnt[:n_q].to(torch.int64)
@@ -140,6 +158,30 @@ class ShardedGallery:
             return self.rank_queries(q_local, gt_csr, n_q, mode, None, return_host, chunks)
         return ranks.cpu().numpy().astype(np.int64)
 
+    def gather_rows_async(self, x_local: torch.Tensor, out: torch.Tensor):
+        """gather_rows_async for this rank's world.  Issue it BEFORE enqueueing the compute that
+        should overlap it -- the collective first waits for the work already on the current stream --
+        and call .wait() on the returned Work before reading `out`."""
+        return gather_rows_async(x_local, out, self.world)
+
+    def rank_queries_device(self, q_all: torch.Tensor, gt_csr, n_q: int, mode: int = _lib.SIM_F16, events=None,
+                            chunks: int = 1):
+        """rank_queries on already-gathered queries with no host synchronisation: returns
+        (ranks int64 [n_q] on the device, overflow flag bool [] on the device).  A set flag means the
+        undecided-pair list overflowed and the counts are incomplete: grow the workspace and redo."""
+        q = engine.RowSet(q_all, with_lo=(mode == _lib.SIM_BF16X3), with_f16=(mode == _lib.SIM_F16),
+                          device=self.device)
+        off, idx = gt_csr
+        sgt, _, _ = engine.gt_thresholds(q, self.shard, off, idx, mode)
+        sgt = merge_gt_scores(sgt, self.world)
+        hi, lo = engine.rank_thresholds(q, self.shard, sgt, mode)
+        cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events,
+                                          chunks=chunks)
+        ch = self.ws.chunks
+        ovf = any_flag((self.ws.count[:ch] > self.ws.cap // ch).any(), self.world)  # every rank redoes together
+        cnt = reduce_counts(cnt, self.world)
+        return ranks_from(cnt, sgt, n_q, self.n_global), ovf
+
     def topk(self, q_local: torch.Tensor, k: int, mode: int = _lib.SIM_F16):
         """Global exact top-k (global ids, fp64 cosines) of all gathered queries."""
         q_all = self.all_gather_rows(q_local)
@@ -149,6 +191,12 @@ class ShardedGallery:
         idx = torch.from_numpy(np.where(idx >= 0, idx + self.offset, -1)).to(self.device)
         sc = torch.from_numpy(sc).to(self.device)
         return merge_topk(idx, sc, k, self.world)
+
+
+def recall_counts_device(ranks: torch.Tensor) -> torch.Tensor:
+    """#(rank <= 1), #(rank <= 5), #(rank <= 10), sum of ranks: int64 [4] on the device (R@K counts
+    without a host round trip; metrics.py:149-157 divides by n_q)."""
+    return torch.stack([(ranks <= 1).sum(), (ranks <= 5).sum(), (ranks <= 10).sum(), ranks.sum()])
 
 
 def metrics_from_ranks(ranks: np.ndarray) -> List[float]:

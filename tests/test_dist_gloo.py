@@ -41,8 +41,10 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         # each rank contributes its query slice; all-gather restores the global order
         q_local = torch.from_numpy(qs[rank * q_per_rank:(rank + 1) * q_per_rank].copy())
         q_all = torch.empty((world * q_per_rank, d), dtype=q_local.dtype)
-        dist.all_gather_into_tensor(q_all, q_local)
+        work = D.gather_rows_async(q_local, q_all, world)  # the bench's overlapped form
+        work.wait()
         assert np.array_equal(q_all.numpy(), qs)
+        assert bool(D.any_flag(torch.tensor(rank == 1), world)) and not bool(D.any_flag(torch.tensor(False), world))
         s = R.exact_scores64(q_all.numpy(), gal[lo:hi])             # local shard scores (oracle)
         local = D.local_gt_lists(gts, lo, hi)
         sgt = torch.tensor([s[i, l].max() if l else np.nan for i, l in enumerate(local)], dtype=torch.float64)
@@ -50,7 +52,10 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         cnt = torch.tensor([int(np.count_nonzero(s[i] > sgt[i].item())) if not np.isnan(sgt[i].item()) else 0
                             for i in range(n_q)], dtype=torch.int32)
         cnt = D.reduce_counts(cnt, world)
-        ranks = D.ranks_from(cnt, sgt, n_q, n_g).numpy()
+        ranks_t = D.ranks_from(cnt, sgt, n_q, n_g)
+        ranks = ranks_t.numpy()
+        rc = D.recall_counts_device(ranks_t).tolist()
+        assert rc == [int((ranks <= 1).sum()), int((ranks <= 5).sum()), int((ranks <= 10).sum()), int(ranks.sum())]
         kk = min(k, hi - lo)
         order = np.argsort(-s, axis=1, kind="stable")[:, :kk]
         idx_g = torch.from_numpy(order + lo)
