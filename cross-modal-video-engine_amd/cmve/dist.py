@@ -178,8 +178,10 @@ class ShardedGallery:
         cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events,
                                           chunks=chunks)
         ch = self.ws.chunks
-        ovf = any_flag((self.ws.count[:ch] > self.ws.cap // ch).any(), self.world)  # every rank redoes together
-        cnt = reduce_counts(cnt, self.world)
+        ovf = (self.ws.count[:ch] > self.ws.cap // ch).any()
+        if self.world > 1:  # the overflow flag rides the counts' all-reduce(SUM): one collective, all ranks agree
+            both = reduce_counts(torch.cat([cnt, ovf.to(cnt.dtype).reshape(1)]), self.world)
+            cnt, ovf = both[:-1], both[-1] > 0
         return ranks_from(cnt, sgt, n_q, self.n_global), ovf
 
     def topk(self, q_local: torch.Tensor, k: int, mode: int = _lib.SIM_F16):
