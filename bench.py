@@ -102,6 +102,54 @@ def msrvtt1ka(steps=20):
             "note": "includes gallery+query packing, GT scoring, both directions, D2H of ranks"}
 
 
+def inference_leg(n_gallery=1048576, d=1024, k=10, reps=20, cpu_rows=262144):
+    """LINAS inference.py scorer (inference.py:76-82: cal_error + argsort[:topK]) at the north star's
+    1M-video gallery on one GPU: exact top-k of single captions (the HBM-bound GEMV regime) and of
+    16-caption batches.  The gallery is packed once (resident); a call = query pack + GEMV + top-k
+    select + fp64 re-score + D2H of the ids.  CPU leg: the oracle port of the reference's per-query
+    path (re-normalise the gallery, fp64 GEMV, full argsort) on a bounded sample of the gallery."""
+    from cmve import engine
+    from oracle import retrieval as R
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gen = torch.Generator(device=dev).manual_seed(77)
+    gal = torch.randn((n_gallery, d), generator=gen, device=dev, dtype=torch.float32)
+    g = engine.RowSet(gal, eps=0.0, with_lo=True, device=dev)
+    picks = torch.randint(0, n_gallery, (32,), generator=gen, device=dev)
+    caps = (gal[picks] + 10.0 * torch.randn((32, d), generator=gen, device=dev)).contiguous()
+    out = {"gallery": n_gallery, "dim": d, "k": k}
+    ws = torch.empty(engine.topk_workspace_floats(engine.RowSet(caps[:16], eps=0.0, with_lo=True, device=dev), g, k),
+                     dtype=torch.float32, device=dev)
+    ids1 = None
+    for nq in (1, 16):
+        times = []
+        for r in range(reps + 3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            q = engine.RowSet(caps[r % 16:r % 16 + nq] if nq == 1 else caps[:nq], eps=0.0, with_lo=True, device=dev)
+            idx, _ = engine.topk(q, g, k, scores_ws=ws)
+            if r >= 3:
+                times.append(time.perf_counter() - t0)
+            if nq == 1 and r == 3:
+                ids1 = (r % 16, idx[0])
+        ms = float(np.median(times)) * 1e3
+        gemv_bytes = n_gallery * g.d_pad * 2  # the fp16 gallery plane, streamed once per call
+        out[f"nq{nq}"] = {"ms_per_call": ms, "pairs_per_s": nq * n_gallery / (ms * 1e-3),
+                          "gallery_GBps_lower_bound": gemv_bytes / (ms * 1e-3) / 1e9}
+    # CPU oracle port of the reference path on a bounded sample (one caption, first cpu_rows videos)
+    g_np = gal[:cpu_rows].cpu().numpy().astype(np.float64)
+    c_np = caps[ids1[0]:ids1[0] + 1].cpu().numpy()
+    t0 = time.perf_counter()
+    top = R.inference_topk(g_np, c_np, k)
+    dt = time.perf_counter() - t0
+    out["cpu_baseline"] = {"value": cpu_rows / dt, "unit": "pairs/s", "kind": "port",
+                           "sample": f"1 caption x {cpu_rows} videos x {d}-d: fp64 l2norm of the gallery, GEMV, "
+                                     f"full argsort (oracle/retrieval.py inference_topk), {dt:.2f} s"}
+    out["gpu_over_cpu_nq1"] = out["nq1"]["pairs_per_s"] / out["cpu_baseline"]["value"]
+    del g, gal
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(gallery_np, queries_np, gts_local, n_sample):
     """Oracle port of the reference CPU path: fp64 cal_error (evaluation.py:17-21) + per-row argsort
     eval_q2m (metrics.py:124-157) on a bounded sample of the same workload."""
@@ -250,6 +298,7 @@ def main():
         }
         if world == 1 and not args.no_extras:
             out["msrvtt1kA"] = msrvtt1ka()
+            out["inference_topk"] = inference_leg()
             if not args.no_cpu_baseline:
                 g_np = gallery.cpu().numpy()
                 q_np = q_local.cpu().numpy()

@@ -328,27 +328,39 @@ def rank_from_matrix(errors, gts, transposed: bool = False, device=None) -> np.n
     return ranks
 
 
-def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Optional[torch.Tensor] = None):
-    """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines."""
+def topk_workspace_floats(q: RowSet, g: RowSet, k: int) -> int:
+    """Floats of device workspace cmve_topk needs for this query set / gallery / k."""
+    n = C.c_int64()
+    check(lib.cmve_topk_workspace(C.byref(q.desc), C.byref(g.desc), int(k), C.byref(n)), "cmve_topk_workspace")
+    return n.value
+
+
+def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Optional[torch.Tensor] = None,
+         to_host: bool = True):
+    """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines.
+    to_host=False returns the device tensors (int32 idx, fp64 scores) instead of numpy arrays."""
     k = int(min(k, g.n))
     if k < 1:
         return np.zeros((q.n, 0), np.int64), np.zeros((q.n, 0))
     if k > _lib.TOPK_MAX:
         raise ValueError(f"topk: k <= {_lib.TOPK_MAX}")
-    if scores_ws is None or scores_ws.numel() < q.n_pad * g.n_pad:
-        scores_ws = torch.empty(q.n_pad * g.n_pad, dtype=torch.float32, device=q.device)
+    need = topk_workspace_floats(q, g, k)
+    if scores_ws is None or scores_ws.numel() < need:
+        scores_ws = torch.empty(need, dtype=torch.float32, device=q.device)
     idx = torch.empty((max(q.n, 1), k), dtype=torch.int32, device=q.device)
     sc = torch.empty((max(q.n, 1), k), dtype=torch.float64, device=q.device)
     ovf = torch.zeros(1, dtype=torch.int32, device=q.device)
     if mode == _lib.SIM_F16 and not (q.has_f16 and g.has_f16):
         mode = _lib.SIM_BF16
     for m in ((mode, _lib.SIM_BF16X3) if (mode != _lib.SIM_BF16X3 and q.has_lo and g.has_lo) else (mode,)):
-        check(lib.cmve_topk(handle(q.device), C.byref(q.desc), C.byref(g.desc), m, k, _ptr(scores_ws), _ptr(idx),
-                            _ptr(sc), _ptr(ovf)), "cmve_topk")
+        check(lib.cmve_topk(handle(q.device), C.byref(q.desc), C.byref(g.desc), m, k, _ptr(scores_ws),
+                            scores_ws.numel(), _ptr(idx), _ptr(sc), _ptr(ovf)), "cmve_topk")
         if int(ovf.item()) == 0:
             break
     else:
         raise _lib.CmveError("topk: the error band kept more than 4096 columns for some query")
+    if not to_host:
+        return idx[:q.n], sc[:q.n]
     return idx[:q.n].to(torch.int64).cpu().numpy(), sc[:q.n].cpu().numpy()
 
 

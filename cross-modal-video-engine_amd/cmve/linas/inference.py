@@ -5,8 +5,9 @@ Reference hot loop (inference.py:76-82):
     inds = np.argsort(errors[0])[:opt.topK]                               # full O(N log N) sort
     print([video_ids[i] for i in inds])
 Here the gallery is normalised and packed into HBM ONCE (``GalleryScorer``) and each
-query batch is scored by the bf16 MFMA kernel with an exact fp64 top-k epilogue
-(``cmve_topk``): same ids, same order (score desc; ties by index) as the reference's
+query batch is scored by ``cmve_topk``: a gallery-streaming fp16 MFMA GEMV for up to 32
+queries (the GEMM beyond), a histogram bound on the k-th score, and an exact fp64 re-score
+of the error band: same ids, same order (score desc; ties by index) as the reference's
 argsort on tie-free scores.
 
 CLI (same flags as inference.py:37-44, plus the inputs the frozen encoder would make):
@@ -44,7 +45,7 @@ class GalleryScorer:
         """[N_q, topK] gallery indices, best first (== np.argsort(cal_error(...)[i])[:topK])."""
         cap_embs = np.atleast_2d(np.asarray(cap_embs))
         q = engine.RowSet(cap_embs, eps=0.0, with_lo=self.gallery.has_lo, device=self.gallery.device)
-        need = q.n_pad * self.gallery.n_pad
+        need = engine.topk_workspace_floats(q, self.gallery, min(topK, self.gallery.n))
         if self._ws is None or self._ws.numel() < need:
             import torch
             self._ws = torch.empty(need, dtype=torch.float32, device=self.gallery.device)

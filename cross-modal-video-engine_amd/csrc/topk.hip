@@ -1,104 +1,339 @@
 // K4(c) + K5: exact top-k per query -- LINAS-engine/inference.py:78-79
 // (errors = cal_error(video_embs, cap_emb); np.argsort(errors[0])[:topK]).
 //
-// 1. sim_store (bf16 MFMA) writes approximate scores s~ into a workspace row.
-// 2. one 1024-thread block per query: 4-pass radix select (8-bit digits on the
-//    order-preserving uint image of the float) finds the k-th largest s~ (T_k); every
-//    column with s~ >= T_k - 2E is kept (E = rigorous score error bound, so the true
-//    top-k is a subset of the kept columns: |T~_k - T_k| <= E).
-// 3. the kept columns are re-scored in fp64 (cos64, same routine as the rank path),
-//    bitonic-sorted in LDS by (score desc, index asc) and the first k written out.
+// 1. approximate scores s~ [n_q, n_g] fp32 into the workspace:
+//      n_q <= 32 : K12a gemv_scores_kernel -- the gallery streamed ONCE from HBM (the fp16 plane,
+//                  2 B per element), 16 gallery rows per wave per MFMA, the (<= 32) query rows
+//                  staged in LDS as the A operand: the inference.py regime (one caption against
+//                  the whole gallery) is an HBM-bound GEMV, not a 256-row GEMM tile
+//      otherwise : K4 sim_store (the G128 / G256 MFMA GEMM)
+// 2. K12b score_hist_kernel: per query a 4096-bin histogram of s~ over [-1, 1] (bin width
+//    2^-11), many blocks per query;
+// 3. K12c topk_thresh_kernel: the bin b* holding the k-th largest s~ gives a lower bound
+//    L <= T~_k; tau = round_down(L - 2E) (E = rigorous score error bound, DESIGN.md s4:
+//    every true top-k column has s~ >= T~_k - 2E >= tau);
+// 4. K12d topk_collect_kernel: columns with s~ >= tau -> a per-query candidate list;
+// 5. K12e topk_finish_kernel: one block per query -- radix select of T~_k over the candidates,
+//    band s~ >= T~_k - 2E, exact fp64 re-score (cos64, the rank path's routine), LDS bitonic
+//    sort (score desc, index asc).  A query whose candidate list overflowed selects over its
+//    dense workspace row instead (same code, dense source): exact either way.
+// The score matrix is read twice by many blocks per query (histogram, collect) instead of
+// five times by one block per query (the 4-pass radix select of the first version).
 #include "cmve_internal.h"
 
 namespace cmve {
 
+typedef _Float16 tk_f16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 tk_bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short tk_s16x8_t __attribute__((ext_vector_type(8)));
+typedef float tk_f32x4_t __attribute__((ext_vector_type(4)));
+
 constexpr int TOPK_THREADS = 1024;
-constexpr int TOPK_CAP = 4096;  // kept columns per query (LDS: 4096 x 12 B)
+constexpr int TOPK_CAP = 4096;   // band columns re-scored per query (LDS: 4096 x 12 B)
+constexpr int CAND_CAP = 8192;   // candidates per query from the histogram threshold (LDS: 8192 x 8 B)
+constexpr int HBINS = 4096;      // histogram bins over [-1, 1]
+constexpr int GEMV_MAX_Q = 32;   // K12a handles up to two 16-row query tiles
+constexpr int GEMV_U = 8;        // k-steps (32 deep each) whose loads are issued together
+constexpr int64_t CHUNK_MIN = 16384;  // histogram / collect columns per block (at least)
 
 __device__ __forceinline__ uint32_t okey(float f) {
   const uint32_t u = __float_as_uint(f);
   if (f != f) return 0u;  // NaN ranks last (np.argsort puts NaN errors last)
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+__device__ __forceinline__ float okey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// monotone non-decreasing bin of a finite-or-infinite score (NaN excluded by the callers)
+__device__ __forceinline__ int score_bin(float s) {
+  const float t = fminf(fmaxf((s + 1.0f) * 2048.0f, 0.0f), (float)(HBINS - 1));
+  return (int)t;
+}
 
-template <typename TQ, typename TG>
-__global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restrict__ scores, int64_t lds_,
-                                                            int64_t ng, int k, const TQ* __restrict__ qraw,
-                                                            int64_t ldq, const double* __restrict__ qinv,
-                                                            const float* __restrict__ qerr,
-                                                            const TG* __restrict__ graw, int64_t ldg,
-                                                            const double* __restrict__ ginv,
-                                                            const float* __restrict__ gerr_max, int64_t d,
-                                                            int64_t d_pad, int mode, int32_t* __restrict__ out_idx,
-                                                            double* __restrict__ out_score,
-                                                            int32_t* __restrict__ overflow) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t sh_prefix, sh_need, sh_count;
-  __shared__ double cs[TOPK_CAP];
-  __shared__ int32_t ci[TOPK_CAP];
+// ---------------------------------------------------------------------------
+// K12a: small-batch scores.  Wave w of block b owns gallery rows [16 (4b + w), +16) (grid-stride);
+// per 32-deep k-step a lane loads 16 B of one gallery row (row = lane & 15, k-chunk = lane >> 4:
+// the B operand of v_mfma_f32_16x16x32) and reads the matching A fragment of each query tile from
+// LDS, stored lane-linear per k-step (conflict-free ds_read_b128).  GEMV_U k-steps of loads are
+// issued before their MFMAs; with ~16 waves per CU that keeps ~128 KiB in flight per CU.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ tk_f32x4_t tk_mfma(tk_s16x8_t a, tk_s16x8_t b, tk_f32x4_t c) {
+  if constexpr (MODE == CMVE_SIM_F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(tk_f16x8_t, a), __builtin_bit_cast(tk_f16x8_t, b),
+                                                  c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(tk_bf16x8_t, a),
+                                                   __builtin_bit_cast(tk_bf16x8_t, b), c, 0, 0, 0);
+}
+
+template <int MODE, int NQT>
+__global__ __launch_bounds__(256) void gemv_scores_kernel(const uint16_t* __restrict__ qhi,
+                                                          const uint16_t* __restrict__ qlo,
+                                                          const uint16_t* __restrict__ ghi,
+                                                          const uint16_t* __restrict__ glo, int64_t d_pad, int nq,
+                                                          int64_t ng, float* __restrict__ ws, int64_t ldw) {
+  constexpr int PL = (MODE == CMVE_SIM_BF16X3) ? 2 : 1;  // planes: hi (+ lo)
+  extern __shared__ tk_s16x8_t qa[];                      // [NQT][PL][nks][64] lane-linear fragments
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t row = blockIdx.x;
-  const float* s = scores + row * lds_;
+  const int nks = (int)(d_pad >> 5);  // 32-deep k-steps
+  // stage the query tiles: fragment (t, p, s, l) = plane p, row 16t + (l & 15), chunk 4s + (l >> 4)
+  const int nfrag = NQT * PL * nks * 64;
+  for (int f = tid; f < nfrag; f += 256) {
+    const int l = f & 63, s = (f >> 6) % nks, tp = (f >> 6) / nks, p = tp % PL, t = tp / PL;
+    const uint16_t* src = (p == 0 ? qhi : qlo) + (int64_t)(16 * t + (l & 15)) * d_pad + (4 * s + (l >> 4)) * 8;
+    qa[f] = *(const tk_s16x8_t*)src;
+  }
+  __syncthreads();
+  const int64_t ngroups = (ng + 15) >> 4;
+  for (int64_t grp = (int64_t)blockIdx.x * 4 + wave; grp < ngroups; grp += (int64_t)gridDim.x * 4) {
+    const int64_t row = grp * 16 + (lane & 15);  // < n_pad (rows padded to 256)
+    const uint16_t* gh = ghi + row * d_pad + (lane >> 4) * 8;
+    const uint16_t* gl = (PL == 2) ? glo + row * d_pad + (lane >> 4) * 8 : nullptr;
+    tk_f32x4_t acc[NQT];
+#pragma unroll
+    for (int t = 0; t < NQT; ++t) acc[t] = tk_f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < nks; s0 += GEMV_U) {
+      tk_s16x8_t bh[GEMV_U], bl[GEMV_U];
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        if (s0 + u < nks) {
+          bh[u] = __builtin_nontemporal_load((const tk_s16x8_t*)(gh + (s0 + u) * 32));
+          if constexpr (PL == 2) bl[u] = __builtin_nontemporal_load((const tk_s16x8_t*)(gl + (s0 + u) * 32));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < GEMV_U; ++u) {
+        if (s0 + u < nks) {
+#pragma unroll
+          for (int t = 0; t < NQT; ++t) {
+            const tk_s16x8_t ah = qa[((t * PL) * nks + s0 + u) * 64 + lane];
+            acc[t] = tk_mfma<MODE>(ah, bh[u], acc[t]);
+            if constexpr (PL == 2) {
+              const tk_s16x8_t al = qa[((t * PL + 1) * nks + s0 + u) * 64 + lane];
+              acc[t] = tk_mfma<MODE>(ah, bl[u], acc[t]);
+              acc[t] = tk_mfma<MODE>(al, bh[u], acc[t]);
+            }
+          }
+        }
+      }
+    }
+    // C[q = 16t + 4 (lane >> 4) + r][j = grp*16 + (lane & 15)]
+    if (row < ng) {
+#pragma unroll
+      for (int t = 0; t < NQT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * t + 4 * (lane >> 4) + r;
+          if (qi < nq) ws[(int64_t)qi * ldw + row] = acc[t][r];
+        }
+    }
+  }
+}
 
-  // ---- radix select of the k-th largest key ----
+// ---------------------------------------------------------------------------
+// K12b: histogram of s~ per query.  grid (nchunk, nq); a block owns columns [c0, c1) of one row.
+// nchunk == 1: the block writes every bin (no pre-zeroing); else nonzero bins are added atomically
+// into a zeroed histogram.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void score_hist_kernel(const float* __restrict__ ws, int64_t ldw, int64_t ng,
+                                                          int64_t chunk, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[HBINS];
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.y;
+  for (int b = tid; b < HBINS; b += 1024) h[b] = 0;
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = min(ng, c0 + chunk);
+  const float* s = ws + q * ldw;
+  // chunk and ldw are multiples of 4 and ws is 16-B aligned: float4 body, scalar tail
+  const int64_t v1 = c0 + ((c1 - c0) & ~(int64_t)3);
+  for (int64_t j = c0 + 4 * (int64_t)tid; j < v1; j += 4 * 1024) {
+    const float4 v = *(const float4*)(s + j);
+    if (v.x == v.x) atomicAdd(&h[score_bin(v.x)], 1u);
+    if (v.y == v.y) atomicAdd(&h[score_bin(v.y)], 1u);
+    if (v.z == v.z) atomicAdd(&h[score_bin(v.z)], 1u);
+    if (v.w == v.w) atomicAdd(&h[score_bin(v.w)], 1u);
+  }
+  for (int64_t j = v1 + tid; j < c1; j += 1024) {
+    const float v = s[j];
+    if (v == v) atomicAdd(&h[score_bin(v)], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = hist + q * HBINS;
+  if (gridDim.x == 1) {
+    for (int b = tid; b < HBINS; b += 1024) out[b] = h[b];
+  } else {
+    for (int b = tid; b < HBINS; b += 1024)
+      if (h[b]) atomicAdd(&out[b], h[b]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K12c: per query, the bin b* where the count from the top first reaches k; L = lower edge of
+// b* minus 2^-20 (covers the fp32 rounding of the bin arithmetic), tau = round_down(L - 2E).
+// Fewer than k finite scores: keep every column (tau = -inf, keepall = 1, NaN included).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void topk_thresh_kernel(const uint32_t* __restrict__ hist, int k,
+                                                          const float* __restrict__ qerr,
+                                                          const float* __restrict__ gerr_max, int slot,
+                                                          int64_t d_pad, int mode, float* __restrict__ tau,
+                                                          int32_t* __restrict__ keepall) {
+  __shared__ uint32_t part[256];
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const uint32_t* h = hist + q * HBINS;
+  // thread t owns bins [HBINS - 16 (t+1), HBINS - 16 t): thread 0 the top of the range
+  const int top = HBINS - 16 * tid;
+  uint32_t mine = 0;
+  for (int b = top - 16; b < top; ++b) mine += h[b];
+  part[tid] = mine;
+  __syncthreads();
+  // inclusive scan (top first), Hillis-Steele in LDS
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  const uint32_t total = part[255];
+  const uint32_t before = tid ? part[tid - 1] : 0u;
+  if (tid == 0 && total < (uint32_t)k) {
+    tau[q] = -INFINITY;
+    keepall[q] = 1;
+  }
+  if (total >= (uint32_t)k && before < (uint32_t)k && before + mine >= (uint32_t)k) {
+    uint32_t acc = before;
+    int b = top - 1;
+    for (; b > top - 16; --b) {
+      acc += h[b];
+      if (acc >= (uint32_t)k) break;
+    }
+    const double E = score_error_bound((double)qerr[q], (double)gerr_max[slot], d_pad, mode);
+    const double L = (b == 0) ? -INFINITY : (double)b / 2048.0 - 1.0 - 0x1p-20;
+    tau[q] = f32_round_down(L - 2.0 * E);
+    keepall[q] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K12d: candidates s~ >= tau[q] -> cand[q][0, CAND_CAP) (the count may exceed the capacity:
+// the finish kernel then selects over the dense row).  One global atomic per wave with a hit.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void topk_collect_kernel(const float* __restrict__ ws, int64_t ldw, int64_t ng,
+                                                           int64_t chunk, const float* __restrict__ tau,
+                                                           const int32_t* __restrict__ keepall,
+                                                           uint32_t* __restrict__ cnt, int32_t* __restrict__ cand) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = blockIdx.y;
+  const float t = tau[q];
+  const bool all = keepall[q] != 0;
+  const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = min(ng, c0 + chunk);
+  const float* s = ws + q * ldw;
+  int32_t* cq = cand + q * CAND_CAP;
+  for (int64_t jb = c0 + (threadIdx.x & ~63); jb < c1; jb += 256) {
+    const int64_t j = jb + lane;
+    const bool keep = j < c1 && (all || s[j] >= t);
+    const uint64_t m = __ballot(keep);
+    if (m == 0) continue;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&cnt[q], (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const uint32_t p = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      if (p < (uint32_t)CAND_CAP) cq[p] = (int32_t)j;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K12e (and the dense fallback): select the k-th largest s~ over a source of (score, column)
+// entries, keep the 2E band, re-score it in fp64, sort, write the first k.
+// ---------------------------------------------------------------------------
+struct DenseSrc {  // one workspace row
+  const float* s;
+  int64_t n;
+  __device__ float score(int64_t c) const { return s[c]; }
+  __device__ int32_t col(int64_t c) const { return (int32_t)c; }
+};
+struct ListSrc {  // candidates staged in LDS
+  const float* s;
+  const int32_t* idx;
+  int64_t n;
+  __device__ float score(int64_t c) const { return s[c]; }
+  __device__ int32_t col(int64_t c) const { return idx[c]; }
+};
+
+struct FinishLds {
+  uint32_t hist[256];
+  uint32_t sh_prefix, sh_need, sh_count;
+  double cs[TOPK_CAP];
+  int32_t ci[TOPK_CAP];
+};
+
+template <class Src, typename TQ, typename TG>
+__device__ void select_rescore_sort(const Src& src, FinishLds& L, int64_t row, int k, const TQ* __restrict__ xq,
+                                    const double qinv, const float qerr, const TG* __restrict__ graw, int64_t ldg,
+                                    const double* __restrict__ ginv, const float gerr_max, int64_t d, int64_t d_pad,
+                                    int mode, int32_t* __restrict__ out_idx, double* __restrict__ out_score,
+                                    int32_t* __restrict__ overflow) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // ---- radix select of the k-th largest key (8-bit digits, 4 passes) ----
   uint32_t prefix = 0, mask = 0, need = (uint32_t)k;
   for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int b = tid; b < 256; b += TOPK_THREADS) hist[b] = 0;
+    for (int b = tid; b < 256; b += TOPK_THREADS) L.hist[b] = 0;
     __syncthreads();
-    for (int64_t j = tid; j < ng; j += TOPK_THREADS) {
-      const uint32_t key = okey(s[j]);
-      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    for (int64_t c = tid; c < src.n; c += TOPK_THREADS) {
+      const uint32_t key = okey(src.score(c));
+      if ((key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
     if (tid == 0) {
       uint32_t acc = 0;
       int b = 255;
       for (; b > 0; --b) {
-        if (acc + hist[b] >= need) break;
-        acc += hist[b];
+        if (acc + L.hist[b] >= need) break;
+        acc += L.hist[b];
       }
-      sh_prefix = prefix | ((uint32_t)b << shift);
-      sh_need = need - acc;
+      L.sh_prefix = prefix | ((uint32_t)b << shift);
+      L.sh_need = need - acc;
     }
     __syncthreads();
-    prefix = sh_prefix;
-    need = sh_need;
+    prefix = L.sh_prefix;
+    need = L.sh_need;
     mask |= 255u << shift;
     __syncthreads();
   }
-  // prefix is now the key of the k-th largest score
+  // prefix is now the key of the k-th largest score (0: fewer than k finite scores)
   const uint32_t kk = prefix;
-  const float tk = __uint_as_float((kk & 0x80000000u) ? (kk & 0x7fffffffu) : ~kk);
-  const double E = score_error_bound((double)qerr[row], (double)gerr_max[mode_slot(mode)], d_pad, mode);
-  const float tau = (kk == 0u) ? -INFINITY : f32_round_down((double)tk - 2.0 * E);
+  const double E = score_error_bound((double)qerr, (double)gerr_max, d_pad, mode);
+  const float tau = (kk == 0u) ? -INFINITY : f32_round_down((double)okey_inv(kk) - 2.0 * E);
 
   // ---- collect the band ----
-  if (tid == 0) sh_count = 0;
+  if (tid == 0) L.sh_count = 0;
   __syncthreads();
-  for (int64_t j = tid; j < ng; j += TOPK_THREADS) {
-    const float v = s[j];
-    if (v >= tau || (kk == 0u)) {  // kk == 0: fewer than k finite scores -> keep everything
-      const uint32_t p = atomicAdd(&sh_count, 1u);
-      if (p < (uint32_t)TOPK_CAP) ci[p] = (int32_t)j;
+  for (int64_t c = tid; c < src.n; c += TOPK_THREADS) {
+    const float v = src.score(c);
+    if (v >= tau || (kk == 0u)) {  // kk == 0: keep everything
+      const uint32_t p = atomicAdd(&L.sh_count, 1u);
+      if (p < (uint32_t)TOPK_CAP) L.ci[p] = src.col(c);
     }
   }
   __syncthreads();
-  const uint32_t cnt_all = sh_count;
+  const uint32_t cnt_all = L.sh_count;
   if (cnt_all > (uint32_t)TOPK_CAP && tid == 0) atomicOr(overflow, 1);
   const int cnt = (int)min(cnt_all, (uint32_t)TOPK_CAP);
 
   // ---- exact fp64 re-score (one wave per kept column) ----
-  const TQ* xq = qraw + row * ldq;
   for (int c = wave; c < cnt; c += TOPK_THREADS / 64) {
-    const int32_t j = ci[c];
-    double v = wave_dot64(xq, graw + (int64_t)j * ldg, d, lane) * (qinv[row] * ginv[j]);
-    if (lane == 0) cs[c] = (v == v) ? v : -INFINITY;
+    const int32_t j = L.ci[c];
+    const double v = wave_dot64(xq, graw + (int64_t)j * ldg, d, lane) * (qinv * ginv[j]);
+    if (lane == 0) L.cs[c] = (v == v) ? v : -INFINITY;
   }
   int npow = 1;
   while (npow < cnt) npow <<= 1;
   for (int c = cnt + tid; c < npow; c += TOPK_THREADS) {
-    cs[c] = -INFINITY;
-    ci[c] = 0x7fffffff;
+    L.cs[c] = -INFINITY;
+    L.ci[c] = 0x7fffffff;
   }
   __syncthreads();
 
@@ -109,15 +344,14 @@ __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restr
         const int lo = 2 * stride * (t / stride) + (t % stride);
         const int hi = lo + stride;
         const bool desc = ((lo & size) == 0);
-        const double a = cs[lo], b = cs[hi];
-        const int32_t ia = ci[lo], ib = ci[hi];
-        // "a before b" in final order
-        const bool a_first = (a > b) || (a == b && ia < ib);
+        const double a = L.cs[lo], b = L.cs[hi];
+        const int32_t ia = L.ci[lo], ib = L.ci[hi];
+        const bool a_first = (a > b) || (a == b && ia < ib);  // "a before b" in the final order
         if (a_first != desc) {
-          cs[lo] = b;
-          cs[hi] = a;
-          ci[lo] = ib;
-          ci[hi] = ia;
+          L.cs[lo] = b;
+          L.cs[hi] = a;
+          L.ci[lo] = ib;
+          L.ci[hi] = ia;
         }
       }
       __syncthreads();
@@ -125,9 +359,95 @@ __global__ __launch_bounds__(TOPK_THREADS) void topk_kernel(const float* __restr
   }
   for (int t = tid; t < k; t += TOPK_THREADS) {
     const bool ok = t < cnt;
-    out_idx[row * k + t] = ok ? ci[t] : -1;
-    out_score[row * k + t] = ok ? cs[t] : NAN;
+    out_idx[row * k + t] = ok ? L.ci[t] : -1;
+    out_score[row * k + t] = ok ? L.cs[t] : NAN;
   }
+}
+
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(TOPK_THREADS) void topk_finish_kernel(
+    const float* __restrict__ ws, int64_t ldw, int64_t ng, int k, const uint32_t* __restrict__ cnt,
+    const int32_t* __restrict__ cand, const TQ* __restrict__ qraw, int64_t ldq, const double* __restrict__ qinv,
+    const float* __restrict__ qerr, const TG* __restrict__ graw, int64_t ldg, const double* __restrict__ ginv,
+    const float* __restrict__ gerr_max, int slot, int64_t d, int64_t d_pad, int mode, int64_t list_cap,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_score, int32_t* __restrict__ overflow) {
+  __shared__ FinishLds L;
+  __shared__ float ls[CAND_CAP];
+  __shared__ int32_t li[CAND_CAP];
+  const int64_t row = blockIdx.x;
+  const float* s = ws + row * ldw;
+  const uint32_t n = cnt[row];
+  const TQ* xq = qraw + row * ldq;
+  if ((int64_t)n <= list_cap) {
+    const int32_t* cq = cand + row * CAND_CAP;
+    for (int c = threadIdx.x; c < (int)n; c += TOPK_THREADS) {
+      const int32_t j = cq[c];
+      li[c] = j;
+      ls[c] = s[j];
+    }
+    __syncthreads();
+    select_rescore_sort(ListSrc{ls, li, (int64_t)n}, L, row, k, xq, qinv[row], qerr[row], graw, ldg, ginv,
+                        gerr_max[slot], d, d_pad, mode, out_idx, out_score, overflow);
+  } else {
+    select_rescore_sort(DenseSrc{s, ng}, L, row, k, xq, qinv[row], qerr[row], graw, ldg, ginv, gerr_max[slot], d,
+                        d_pad, mode, out_idx, out_score, overflow);
+  }
+}
+
+// workspace layout (in 4-byte units, sections 256-B aligned) for n_q queries over a gallery of n_pad rows
+struct TopkWs {
+  int64_t scores, hist, tau, keepall, cnt, cand, total;
+};
+static inline int64_t al64(int64_t x) { return (x + 63) & ~(int64_t)63; }
+static TopkWs topk_ws_layout(int64_t nq, int64_t g_n_pad) {
+  TopkWs w;
+  w.scores = 0;
+  w.hist = al64(nq * g_n_pad);
+  w.tau = w.hist + al64(nq * HBINS);
+  w.keepall = w.tau + al64(nq);
+  w.cnt = w.keepall + al64(nq);
+  w.cand = w.cnt + al64(nq);
+  w.total = w.cand + al64(nq * CAND_CAP);
+  return w;
+}
+
+template <int MODE>
+static int launch_gemv(const cmve_rows_t* q, const cmve_rows_t* g, float* ws, hipStream_t stream) {
+  constexpr int PL = (MODE == CMVE_SIM_BF16X3) ? 2 : 1;
+  const uint16_t* qh = MODE == CMVE_SIM_F16 ? q->h16 : q->hi;
+  const uint16_t* gh = MODE == CMVE_SIM_F16 ? g->h16 : g->hi;
+  const int nqt = q->n <= 16 ? 1 : 2;
+  const size_t lds = (size_t)nqt * PL * 16 * g->d_pad * 2;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    CMVE_HIP(hipGetDevice(&dev));
+    CMVE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int64_t groups = (g->n + 15) / 16;
+  // enough blocks for ~16 waves per CU, never more than one 16-row group per wave
+  const unsigned nblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 3) / 4, (int64_t)cus * 4));
+#define GV(NQT)                                                                                                     \
+  do {                                                                                                              \
+    static bool attr = false;                                                                                       \
+    if (!attr) {                                                                                                    \
+      CMVE_HIP(hipFuncSetAttribute((const void*)gemv_scores_kernel<MODE, NQT>,                                      \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                        \
+      attr = true;                                                                                                  \
+    }                                                                                                               \
+    hipLaunchKernelGGL((gemv_scores_kernel<MODE, NQT>), dim3(nblocks), dim3(256), lds, stream, qh, q->lo, gh, g->lo, \
+                       g->d_pad, (int)q->n, g->n, ws, g->n_pad);                                                    \
+  } while (0)
+  if (nqt == 1) GV(1);
+  else GV(2);
+#undef GV
+  return check_launch("gemv_scores_kernel");
+}
+
+static bool gemv_fits(const cmve_rows_t* q, const cmve_rows_t* g, int mode) {
+  const int nqt = q->n <= 16 ? 1 : 2;
+  const size_t lds = (size_t)nqt * (mode == CMVE_SIM_BF16X3 ? 2 : 1) * 16 * g->d_pad * 2;
+  return q->n <= GEMV_MAX_Q && lds <= 160 * 1024;
 }
 
 }  // namespace cmve
@@ -137,26 +457,90 @@ using namespace cmve;
 extern "C" int cmve_sim_store(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, float alpha,
                               float beta, void* out, int32_t out_dtype, int64_t ldo);
 
+extern "C" int cmve_topk_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* n_floats) {
+  CMVE_REQUIRE(q && g && n_floats, "cmve_topk_workspace: NULL argument");
+  CMVE_REQUIRE(k >= 1 && k <= TOPK_CAP / 2, "cmve_topk_workspace: k must be in [1, %d]", TOPK_CAP / 2);
+  *n_floats = topk_ws_layout(std::max<int64_t>(q->n, 1), g->n_pad).total;
+  return CMVE_OK;
+}
+
 extern "C" int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
-                         float* scores_ws, int32_t* out_idx, double* out_score, int32_t* overflow) {
+                         float* scores_ws, int64_t ws_floats, int32_t* out_idx, double* out_score,
+                         int32_t* overflow) {
   CMVE_REQUIRE(h && q && g && scores_ws && out_idx && out_score && overflow, "cmve_topk: NULL argument");
   CMVE_REQUIRE(k >= 1, "cmve_topk: k must be >= 1");
   CMVE_REQUIRE(k <= TOPK_CAP / 2, "cmve_topk: k must be <= %d", TOPK_CAP / 2);
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_topk: raw rows / norms missing");
+  CMVE_REQUIRE(q->d == g->d && q->d_pad == g->d_pad && q->d_pad % 64 == 0, "cmve_topk: dimension mismatch");
+  CMVE_REQUIRE(g->n < (1ll << 31), "cmve_topk: gallery too large for int32 indices");
+  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16, "cmve_topk: unknown mode %d",
+               mode);
   CMVE_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), h->stream));
   if (q->n == 0) return CMVE_OK;
-  int st = cmve_sim_store(h, q, g, mode, 1.0f, 0.0f, scores_ws, CMVE_F32, g->n_pad);
-  if (st) return st;
+  const TopkWs w = topk_ws_layout(q->n, g->n_pad);
+  CMVE_REQUIRE(ws_floats >= w.total, "cmve_topk: workspace has %lld floats, needs %lld (cmve_topk_workspace)",
+               (long long)ws_floats, (long long)w.total);
   const float* qerr = mode_err(q, mode);
-  CMVE_REQUIRE(qerr, "cmve_topk: set has no error plane for this mode");
-#define TK(TQ, TG)                                                                                                \
-  hipLaunchKernelGGL((topk_kernel<TQ, TG>), dim3((unsigned)q->n), dim3(TOPK_THREADS), 0, h->stream, scores_ws,    \
-                     g->n_pad, g->n, k, (const TQ*)q->raw, q->raw_ld, q->inv_norm, qerr, (const TG*)g->raw,       \
-                     g->raw_ld, g->inv_norm, g->err_max, q->d, q->d_pad, mode, out_idx, out_score, overflow)
+  CMVE_REQUIRE(qerr && g->err_max, "cmve_topk: set has no error plane for this mode");
+  CMVE_REQUIRE(mode != CMVE_SIM_F16 || (q->h16 && g->h16), "cmve_topk: F16 needs h16 planes");
+  CMVE_REQUIRE(mode != CMVE_SIM_BF16X3 || (q->lo && g->lo), "cmve_topk: BF16X3 needs lo planes");
+  hipStream_t st = h->stream;
+  float* scores = scores_ws + w.scores;
+  uint32_t* hist = (uint32_t*)(scores_ws + w.hist);
+  float* tau = scores_ws + w.tau;
+  int32_t* keepall = (int32_t*)(scores_ws + w.keepall);
+  uint32_t* cnt = (uint32_t*)(scores_ws + w.cnt);
+  int32_t* cand = (int32_t*)(scores_ws + w.cand);
+  if (g->n == 0) {
+    CMVE_HIP(hipMemsetAsync(out_idx, 0xff, sizeof(int32_t) * q->n * k, st));
+    return CMVE_OK;
+  }
+
+  // 1. approximate scores
+  int rc;
+  if (gemv_fits(q, g, mode)) {
+    if (mode == CMVE_SIM_F16) rc = launch_gemv<CMVE_SIM_F16>(q, g, scores, st);
+    else if (mode == CMVE_SIM_BF16) rc = launch_gemv<CMVE_SIM_BF16>(q, g, scores, st);
+    else rc = launch_gemv<CMVE_SIM_BF16X3>(q, g, scores, st);
+  } else {
+    rc = cmve_sim_store(h, q, g, mode, 1.0f, 0.0f, scores, CMVE_F32, g->n_pad);
+  }
+  if (rc) return rc;
+
+  // 2-4. histogram -> threshold -> candidates
+  const int64_t want = std::max<int64_t>(1, 1024 / q->n);
+  const int64_t max_chunks = std::max<int64_t>(1, (g->n + CHUNK_MIN - 1) / CHUNK_MIN);
+  const int64_t nchunk = std::min(want, max_chunks);
+  const int64_t chunk = (((g->n + nchunk - 1) / nchunk) + 255) & ~(int64_t)255;
+  const int64_t nch = (g->n + chunk - 1) / chunk;
+  if (nch > 1) CMVE_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * q->n * HBINS, st));
+  CMVE_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * q->n, st));
+  hipLaunchKernelGGL(score_hist_kernel, dim3((unsigned)nch, (unsigned)q->n), dim3(1024), 0, st, scores, g->n_pad,
+                     g->n, chunk, hist);
+  rc = check_launch("score_hist_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(topk_thresh_kernel, dim3((unsigned)q->n), dim3(256), 0, st, hist, k, qerr, g->err_max,
+                     mode_slot(mode), g->d_pad, mode, tau, keepall);
+  rc = check_launch("topk_thresh_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(topk_collect_kernel, dim3((unsigned)nch, (unsigned)q->n), dim3(256), 0, st, scores, g->n_pad,
+                     g->n, chunk, tau, keepall, cnt, cand);
+  rc = check_launch("topk_collect_kernel");
+  if (rc) return rc;
+
+  // 5. select + exact re-score + sort.  CMVE_TOPK_DENSE=1 (tests only) sends every query down the
+  // dense-row path that a candidate-list overflow takes.
+  const char* dense_env = getenv("CMVE_TOPK_DENSE");
+  const int64_t list_cap = (dense_env && atoi(dense_env)) ? -1 : CAND_CAP;
+#define TK(TQ, TG)                                                                                                 \
+  hipLaunchKernelGGL((topk_finish_kernel<TQ, TG>), dim3((unsigned)q->n), dim3(TOPK_THREADS), 0, st, scores,       \
+                     g->n_pad, g->n, k, cnt, cand, (const TQ*)q->raw, q->raw_ld, q->inv_norm, qerr,                \
+                     (const TG*)g->raw, g->raw_ld, g->inv_norm, g->err_max, mode_slot(mode), q->d, q->d_pad, mode, \
+                     list_cap, out_idx, out_score, overflow)
   if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) TK(float, float);
   else if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F64) TK(float, double);
   else if (q->raw_dtype == CMVE_F64 && g->raw_dtype == CMVE_F32) TK(double, float);
   else TK(double, double);
 #undef TK
-  return check_launch("topk_kernel");
+  return check_launch("topk_finish_kernel");
 }

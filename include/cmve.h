@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 3
+#define CMVE_ABI_VERSION 4
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -315,17 +315,23 @@ int cmve_gt_positions_from_matrix(cmve_handle_t h, const void* errors, int32_t d
 
 /*
  * K4(c) -- exact top-k per query (LINAS-engine/inference.py:78-79:
- * np.argsort(errors[0])[:topK]).  The MFMA pass writes approximate scores into
- * `scores_ws` [q->n_pad, g->n_pad] fp32; one block per query radix-selects the
- * k-th score and keeps every column within 2E of it (E = rigorous score error
- * bound; at most 4096 per query), re-scores them in fp64 and sorts them
+ * np.argsort(errors[0])[:topK]).  Approximate scores s~ go to the workspace: for
+ * q->n <= 32 a gallery-streaming MFMA GEMV (the inference.py regime: one caption
+ * against the whole gallery, HBM-bound), else the MFMA GEMM.  A per-query
+ * histogram of s~ bounds the k-th largest score T~_k from below; every column
+ * within 2E of that bound (E = rigorous score error bound) is a candidate; one
+ * block per query selects T~_k among the candidates, keeps the band
+ * s~ >= T~_k - 2E (at most 4096 columns), re-scores it in fp64 and sorts it
  * (score desc, index asc).  out_idx [q->n, k] int32, out_score [q->n, k] fp64
- * (the exact cosine).  *overflow (device int32) becomes non-zero if a query kept
- * more than 4096 columns (retry with CMVE_SIM_BF16X3, whose band is ~10x narrower).
- * 1 <= k <= 2048.
+ * (the exact cosine).  *overflow (device int32) becomes non-zero if a query's
+ * band kept more than 4096 columns (retry with CMVE_SIM_BF16X3, whose band is
+ * ~10x narrower).  1 <= k <= 2048.
+ * scores_ws: device workspace of at least cmve_topk_workspace() floats
+ * (ws_floats); its first q->n x g->n_pad floats hold s~ row-major.
  */
+int cmve_topk_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* n_floats);
 int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
-              float* scores_ws, int32_t* out_idx, double* out_score, int32_t* overflow);
+              float* scores_ws, int64_t ws_floats, int32_t* out_idx, double* out_score, int32_t* overflow);
 
 /* ---- non-cosine measures ---------------------------------
  * K10: out[i, j] = alpha * f(A_i, B_j) + beta over all pairs, fp64 accumulation.
