@@ -335,15 +335,63 @@ def topk_workspace_floats(q: RowSet, g: RowSet, k: int) -> int:
     return n.value
 
 
+TOPK_BATCH_MIN_Q = 512   # below this the dense score block is small: cmve_topk
+TOPK_BATCH_MAX_K = 128
+
+
+def topk_batch_plan(q: RowSet, g: RowSet, k: int):
+    """(use_batch, sample_rows, workspace_floats) of cmve_topk_batch for this problem: the fused
+    path pays off when the sample it scores densely is at most a quarter of the gallery."""
+    if q.n < TOPK_BATCH_MIN_Q or not 1 <= k <= TOPK_BATCH_MAX_K or g.n >= (1 << 24):
+        return False, 0, 0
+    ns, nf = C.c_int64(), C.c_int64()
+    check(lib.cmve_topk_batch_workspace(C.byref(q.desc), C.byref(g.desc), int(k), C.byref(ns), C.byref(nf)),
+          "cmve_topk_batch_workspace")
+    return 4 * ns.value <= g.n, ns.value, nf.value
+
+
+def topk_batch(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, ws: Optional[torch.Tensor] = None):
+    """cmve_topk_batch on device: (idx int32 [n, k], fp64 scores [n, k], unresolved int32 [1]).
+    Rows left unresolved hold idx -2 (topk() finishes them through cmve_topk)."""
+    ok, _, need = topk_batch_plan(q, g, k)
+    if not ok:
+        raise ValueError("topk_batch: problem outside the batch path (see topk_batch_plan)")
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.float32, device=q.device)
+    idx = torch.empty((q.n, k), dtype=torch.int32, device=q.device)
+    sc = torch.empty((q.n, k), dtype=torch.float64, device=q.device)
+    unres = torch.zeros(1, dtype=torch.int32, device=q.device)
+    check(lib.cmve_topk_batch(handle(q.device), C.byref(q.desc), C.byref(g.desc), int(mode), int(k), _ptr(ws),
+                              ws.numel(), _ptr(idx), _ptr(sc), _ptr(unres)), "cmve_topk_batch")
+    return idx, sc, unres
+
+
 def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Optional[torch.Tensor] = None,
-         to_host: bool = True):
+         to_host: bool = True, batch: Optional[bool] = None):
     """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines.
-    to_host=False returns the device tensors (int32 idx, fp64 scores) instead of numpy arrays."""
+    to_host=False returns the device tensors (int32 idx, fp64 scores) instead of numpy arrays.
+    Large query batches go through cmve_topk_batch (no score matrix; batch=False forces the
+    dense path); rows it leaves unresolved are finished by cmve_topk."""
     k = int(min(k, g.n))
     if k < 1:
         return np.zeros((q.n, 0), np.int64), np.zeros((q.n, 0))
     if k > _lib.TOPK_MAX:
         raise ValueError(f"topk: k <= {_lib.TOPK_MAX}")
+    if mode == _lib.SIM_F16 and not (q.has_f16 and g.has_f16):
+        mode = _lib.SIM_BF16
+    use_batch = topk_batch_plan(q, g, k)[0] if batch is None else bool(batch)
+    if use_batch:
+        idx, sc, unres = topk_batch(q, g, k, mode, ws=scores_ws)
+        if int(unres.item()):
+            rows = torch.nonzero(idx[:, 0] == -2).flatten()
+            sub = RowSet(q.raw.index_select(0, rows), eps=q.eps, with_lo=q.has_lo, device=q.device,
+                         with_f16=q.has_f16)
+            i2, s2 = topk(sub, g, k, mode, to_host=False, batch=False)
+            idx[rows] = i2
+            sc[rows] = s2
+        if not to_host:
+            return idx, sc
+        return idx.to(torch.int64).cpu().numpy(), sc.cpu().numpy()
     need = topk_workspace_floats(q, g, k)
     if scores_ws is None or scores_ws.numel() < need:
         scores_ws = torch.empty(need, dtype=torch.float32, device=q.device)

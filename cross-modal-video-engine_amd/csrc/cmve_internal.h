@@ -115,6 +115,17 @@ __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB*
   return wave_sum(acc);
 }
 
+// order-preserving uint32 key of an fp32 score (larger score -> larger key); NaN -> 0 (ranks
+// last, as np.argsort puts NaN errors last)
+__device__ __forceinline__ uint32_t topk_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if (f != f) return 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float topk_key_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
 // fp64 -> fp32 with directed rounding
 __device__ __forceinline__ float f32_round_up(double x) {
   float f = (float)x;

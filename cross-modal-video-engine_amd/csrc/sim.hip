@@ -4,6 +4,8 @@
 //   EPI_RANK   : per-row and per-column "score > threshold" counts + undecided-pair list
 //                (the GT rank of LINAS-engine/util/metrics.py:137-147 without the matrix)
 //   EPI_LINEAR : BN(resid + act(x.w + bias))               (MFC / Combiner projections)
+//   EPI_TOPK   : the RANK epilogue with thresholds (+inf, tau): every s >= tau emitted as a
+//                (score key, row, column) entry, bucketed by 256-row QUERY tile (topk.hip K13)
 //
 // Geometry (template WM x WN waves, each wave TM x 4 tiles of v_mfma_f32_16x16x32):
 //   G128: 2 x 2 waves, 64 x 64 per wave  -> 128 x 128 block tile, 256 threads, 2 blocks / CU
@@ -27,7 +29,9 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int BK = 64;
-constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2;
+constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2, EPI_TOPK = 3;
+// epilogues that count / emit against per-row and per-column thresholds
+constexpr bool epi_thr(int e) { return e == EPI_RANK || e == EPI_TOPK; }
 constexpr int CAND_LDS = 1024;  // per-block undecided-pair buffer (one global atomic per block)
 
 struct SimArgs {
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
                                          (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
 
-  __shared__ EpiLds<BM, BN, EPI == EPI_RANK> epi;
+  __shared__ EpiLds<BM, BN, epi_thr(EPI)> epi;
   int* lds_rc = epi.rc;
   int* lds_cc = epi.cc;
   unsigned long long* lds_cand = epi.cand;
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       lo = a.col_lo[no + tid - BM];
     }
   };
-  if constexpr (EPI == EPI_RANK) {
+  if constexpr (epi_thr(EPI)) {
     static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
     if (tid == 0) *lds_ncand = 0u;
@@ -513,14 +517,28 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           while (m) {
             const int bit = __builtin_ctz(m);
             m &= m - 1u;
-            const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
-            const unsigned long long packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
-                                              ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
+            unsigned long long packed;
+            if constexpr (EPI == EPI_TOPK) {
+              // key(s) << 32 | (row & 255) << 24 | col: the bucket (m0 >> 8) holds the row's high bits
+              float sc = acc[i][0][0];
+  #pragma unroll
+              for (int jj = 0; jj < TN; ++jj)
+  #pragma unroll
+                for (int r = 0; r < 4; ++r) sc = (bit == jj * 4 + r) ? acc[i][jj][r] : sc;
+              packed = ((unsigned long long)topk_key(sc) << 32) |
+                       ((unsigned long long)((rbase + i * 16 + (bit & 3)) & 255) << 24) |
+                       (unsigned long long)(cbase + (bit >> 2) * 16);
+            } else {
+              const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
+              packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
+                       ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
+            }
             if (base < (uint32_t)CAND_LDS) {
               lds_cand[base] = packed;
             } else {  // block buffer full: straight to the tile's bucket
-              const unsigned long long slot = atomicAdd(a.bucket_cnt + (n0 >> CAND_BUCKET_SHIFT), 1ull);
-              if ((long long)slot < a.cap_b) a.cand[(size_t)(n0 >> CAND_BUCKET_SHIFT) * a.cap_b + slot] = packed;
+              const int bk = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
+              const unsigned long long slot = atomicAdd(a.bucket_cnt + bk, 1ull);
+              if ((long long)slot < a.cap_b) a.cand[(size_t)bk * a.cap_b + slot] = packed;
             }
             ++base;
           }
@@ -535,7 +553,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       CMVE_BAR_LDS();
       // flush the block's undecided pairs with ONE global atomic
       const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
-      const int bucket = n0 >> CAND_BUCKET_SHIFT;  // a tile never straddles buckets (BN <= 256)
+      // a tile never straddles buckets (BM, BN <= 256, aligned)
+      const int bucket = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
       if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)nlds);
       CMVE_BAR_LDS();
       for (unsigned t = tid; t < nlds; t += NT) {
@@ -697,7 +716,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       rA = rsrc_of(a.qhi, m0n, BM);
       rB = rsrc_of(a.ghi, n0n, BN);
       prologue_loads();
-      if constexpr (EPI == EPI_RANK) fetch_thr(m0n, n0n, thn_hi, thn_lo);
+      if constexpr (epi_thr(EPI)) fetch_thr(m0n, n0n, thn_hi, thn_lo);
     }
     epilogue();
     if (!has_next) break;
@@ -941,6 +960,26 @@ static int rank_pass(const SimArgs& a, const cmve_rows_t* q, const cmve_rows_t* 
   if (st) return st;
   return launch_cand_finalize(s, g, cand, cand_cap, cand_count);
 }
+
+namespace cmve {
+// K13 main pass (topk.hip): the TOPK epilogue over the whole gallery with per-row thresholds
+// (hi, lo) = (+inf, tau); entries land in cand[nb + b * cap_b ...], b = query row >> 8, counters
+// in cand[0, nb) (zeroed by the caller)
+int launch_topk_gemm(hipStream_t s, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, const float* row_hi,
+                     const float* row_lo, uint64_t* cand, int64_t nb, int64_t cap_b) {
+  int st = validate_pair(q, g, mode, "cmve_topk_batch");
+  if (st) return st;
+  CMVE_REQUIRE(q->n_pad <= (int64_t)nb * 256, "cmve_topk_batch: bucket count too small");
+  CMVE_REQUIRE(g->n < (1ll << 24), "cmve_topk_batch: gallery shard must hold < 2^24 rows");
+  SimArgs a = make_args(q, g, mode);
+  a.row_hi = row_hi;
+  a.row_lo = row_lo;
+  a.bucket_cnt = (unsigned long long*)cand;
+  a.cand = (unsigned long long*)(cand + nb);
+  a.cap_b = cap_b;
+  return dispatch<EPI_TOPK>(a, q, g, mode, s);
+}
+}  // namespace cmve
 
 extern "C" int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs,
                               const float* row_hi, const float* row_lo, const float* col_hi, const float* col_lo,

@@ -36,14 +36,8 @@ constexpr int GEMV_MAX_Q = 32;   // K12a handles up to two 16-row query tiles
 constexpr int GEMV_U = 8;        // k-steps (32 deep each) whose loads are issued together
 constexpr int64_t CHUNK_MIN = 16384;  // histogram / collect columns per block (at least)
 
-__device__ __forceinline__ uint32_t okey(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if (f != f) return 0u;  // NaN ranks last (np.argsort puts NaN errors last)
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float okey_inv(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
+__device__ __forceinline__ uint32_t okey(float f) { return topk_key(f); }
+__device__ __forceinline__ float okey_inv(uint32_t k) { return topk_key_inv(k); }
 // monotone non-decreasing bin of a finite-or-infinite score (NaN excluded by the callers)
 __device__ __forceinline__ int score_bin(float s) {
   const float t = fminf(fmaxf((s + 1.0f) * 2048.0f, 0.0f), (float)(HBINS - 1));
@@ -444,6 +438,180 @@ static int launch_gemv(const cmve_rows_t* q, const cmve_rows_t* g, float* ws, hi
   return check_launch("gemv_scores_kernel");
 }
 
+// ---------------------------------------------------------------------------
+// K13: large-batch top-k without the score matrix (the C5 regime: 16,384 captions x a 131,072-row
+// shard).  tau_i comes from a gallery SAMPLE (its first n_s rows): the k-th largest s~ of a subset
+// is <= the k-th largest over the whole gallery, so tau_i = round_down(L_i - 2E) (K12c on the
+// sample's histogram) is a valid candidate threshold for the full gallery (top-k).
+// The main GEMM (sim.hip EPI_TOPK) then emits every s~ >= tau_i as (key(s~), row & 255, col),
+// bucketed by 256-row query tile; K13b turns each query's entries into its exact top-k.
+// ---------------------------------------------------------------------------
+constexpr int BT_Q = 16;       // queries per finish block (one wave each)
+constexpr int BT_LCAP = 512;   // entries kept per query (more: the row is left to the dense path)
+constexpr int BT_BAND = 256;   // band entries re-scored per query
+constexpr int BT_KMAX = 128;
+constexpr int BT_TARGET = 128; // expected entries per query the sample size is chosen for
+
+__global__ __launch_bounds__(256) void topk_batch_thr_kernel(const float* __restrict__ tau,
+                                                             const int32_t* __restrict__ keepall, int64_t nq,
+                                                             int64_t nq_pad, float* __restrict__ hi,
+                                                             float* __restrict__ lo) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nq_pad) return;
+  const bool ok = r < nq && !keepall[r] && tau[r] > -INFINITY && tau[r] < INFINITY;
+  hi[r] = ok ? INFINITY : __builtin_nanf("");  // NaN: the row emits nothing (left to the dense path)
+  lo[r] = ok ? tau[r] : __builtin_nanf("");
+}
+
+struct BatchLds {
+  uint32_t key[BT_Q][BT_LCAP];
+  int32_t col[BT_Q][BT_LCAP];
+  double bs[BT_Q][BT_BAND];
+  uint32_t cnt[BT_Q];
+  int32_t nband[BT_Q];
+};
+
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(1024) void topk_batch_finish_kernel(
+    const unsigned long long* __restrict__ bucket_cnt, const unsigned long long* __restrict__ cand, int64_t cap_b,
+    int64_t nq, int k, const int32_t* __restrict__ keepall, const TQ* __restrict__ qraw, int64_t ldq,
+    const double* __restrict__ qinv, const float* __restrict__ qerr, const TG* __restrict__ graw, int64_t ldg,
+    const double* __restrict__ ginv, const float* __restrict__ gerr_max, int slot, int64_t d, int64_t d_pad, int mode,
+    int32_t* __restrict__ out_idx, double* __restrict__ out_score, int32_t* __restrict__ unresolved) {
+  __shared__ BatchLds L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // XCD-aware order: the 16 blocks reading one bucket run on one XCD (its entries stay in that L2)
+  const int total = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int xcd = bid & 7, local = bid >> 3, qq = total >> 3, rr = total & 7;
+  const int lb = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + local;
+  const int64_t q0 = (int64_t)lb * BT_Q;
+  const int64_t bucket = q0 >> 8;
+  if (tid < BT_Q) L.cnt[tid] = 0;
+  __syncthreads();
+  const unsigned long long nb_all = bucket_cnt[bucket];
+  const bool bucket_ovf = nb_all > (unsigned long long)cap_b;
+  const int64_t ne = (int64_t)min(nb_all, (unsigned long long)cap_b);
+  const unsigned long long* e = cand + bucket * cap_b;
+  const uint32_t r_lo = (uint32_t)(q0 & 255);
+  for (int64_t t = tid; t < ne; t += 1024) {
+    const unsigned long long v = e[t];
+    const uint32_t rl = (uint32_t)(v >> 24) & 255u;
+    if (rl - r_lo < (uint32_t)BT_Q) {
+      const uint32_t p = atomicAdd(&L.cnt[rl - r_lo], 1u);
+      if (p < (uint32_t)BT_LCAP) {
+        L.key[rl - r_lo][p] = (uint32_t)(v >> 32);
+        L.col[rl - r_lo][p] = (int32_t)(v & 0xffffffu);
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t row = q0 + w;
+  const uint32_t n_all = L.cnt[w];
+  const int m = (int)min(n_all, (uint32_t)BT_LCAP);
+  bool ok = row < nq && !bucket_ovf && !keepall[row] && n_all <= (uint32_t)BT_LCAP && m >= k;
+  // pad to BT_LCAP, then a block-wide bitonic sort of every wave's (key, col) row, key descending
+  for (int t = m + lane; t < BT_LCAP; t += 64) {
+    L.key[w][t] = 0u;
+    L.col[w][t] = 0x7fffffff;
+  }
+  __syncthreads();
+  for (int size = 2; size <= BT_LCAP; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = lane; t < BT_LCAP / 2; t += 64) {
+        const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const uint32_t ka = L.key[w][lo], kb = L.key[w][hi];
+        const int32_t ia = L.col[w][lo], ib = L.col[w][hi];
+        const bool a_first = ka > kb || (ka == kb && ia < ib);
+        if (a_first != desc) {
+          L.key[w][lo] = kb;
+          L.key[w][hi] = ka;
+          L.col[w][lo] = ib;
+          L.col[w][hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // band: the sorted prefix with s~ >= round_down(T~_k - 2E); fp64 re-score (cos64, K5's routine)
+  int nb = 0;
+  if (ok) {
+    const double E = score_error_bound((double)qerr[row], (double)gerr_max[slot], d_pad, mode);
+    const float thr = f32_round_down((double)topk_key_inv(L.key[w][k - 1]) - 2.0 * E);
+    const uint32_t kthr = topk_key(thr);
+    for (int t0 = 0; t0 < m; t0 += 64) {
+      const int t = t0 + lane;
+      const bool in = t < m && L.key[w][t] >= kthr;
+      nb += __popcll(__ballot(in));
+    }
+    if (nb > BT_BAND) ok = false;
+  }
+  if (ok) {
+    const TQ* xq = qraw + row * ldq;
+    const double qi = qinv[row];
+    for (int t = 0; t < nb; ++t) {
+      const int32_t j = L.col[w][t];
+      const double v = wave_dot64(xq, graw + (int64_t)j * ldg, d, lane) * (qi * ginv[j]);
+      if (lane == 0) L.bs[w][t] = (v == v) ? v : -INFINITY;
+    }
+  } else {
+    nb = 0;
+  }
+  for (int t = nb + lane; t < BT_BAND; t += 64) {
+    L.bs[w][t] = -INFINITY;
+    L.col[w][t] = 0x7fffffff;
+  }
+  __syncthreads();
+  // band sort: fp64 score descending, column ascending (the dense path's order)
+  for (int size = 2; size <= BT_BAND; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = lane; t < BT_BAND / 2; t += 64) {
+        const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+        const bool desc = (lo & size) == 0;
+        const double a = L.bs[w][lo], b = L.bs[w][hi];
+        const int32_t ia = L.col[w][lo], ib = L.col[w][hi];
+        const bool a_first = a > b || (a == b && ia < ib);
+        if (a_first != desc) {
+          L.bs[w][lo] = b;
+          L.bs[w][hi] = a;
+          L.col[w][lo] = ib;
+          L.col[w][hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (row < nq) {
+    for (int t = lane; t < k; t += 64) {
+      out_idx[row * k + t] = ok ? L.col[w][t] : -2;  // -2: unresolved, the caller's dense pass
+      out_score[row * k + t] = ok ? L.bs[w][t] : NAN;
+    }
+    if (!ok && lane == 0) atomicAdd(unresolved, 1);
+  }
+}
+
+// workspace of cmve_topk_batch (4-byte units, sections 256-B aligned)
+struct BatchWs {
+  int64_t ns, ns_pad, sc, hist, tau, keepall, hi, lo, cand, nb, cap_b, total;
+};
+static BatchWs batch_ws_layout(int64_t nq, int64_t nq_pad, int64_t g_n, int64_t g_n_pad, int k) {
+  BatchWs w;
+  const int64_t want = ((int64_t)k * g_n + BT_TARGET - 1) / BT_TARGET;
+  w.ns = std::min<int64_t>(g_n, std::max<int64_t>(want, 2 * (int64_t)k));
+  w.ns_pad = std::min<int64_t>(g_n_pad, (w.ns + 255) & ~(int64_t)255);
+  w.sc = 0;
+  w.hist = al64(nq * w.ns_pad);
+  w.tau = w.hist + al64(nq * HBINS);
+  w.keepall = w.tau + al64(nq);
+  w.hi = w.keepall + al64(nq);
+  w.lo = w.hi + al64(nq_pad);
+  w.cand = w.lo + al64(nq_pad);
+  w.nb = (nq_pad + 255) / 256;
+  w.cap_b = 256 * (int64_t)BT_LCAP;
+  w.total = w.cand + 2 * (w.nb + w.nb * w.cap_b);
+  return w;
+}
+
 static bool gemv_fits(const cmve_rows_t* q, const cmve_rows_t* g, int mode) {
   const int nqt = q->n <= 16 ? 1 : 2;
   const size_t lds = (size_t)nqt * (mode == CMVE_SIM_BF16X3 ? 2 : 1) * 16 * g->d_pad * 2;
@@ -543,4 +711,92 @@ extern "C" int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_
   else TK(double, double);
 #undef TK
   return check_launch("topk_finish_kernel");
+}
+
+namespace cmve {
+int launch_topk_gemm(hipStream_t s, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, const float* row_hi,
+                     const float* row_lo, uint64_t* cand, int64_t nb, int64_t cap_b);
+}
+
+extern "C" int cmve_topk_batch_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* sample_rows,
+                                         int64_t* n_floats) {
+  CMVE_REQUIRE(q && g && n_floats, "cmve_topk_batch_workspace: NULL argument");
+  CMVE_REQUIRE(k >= 1 && k <= BT_KMAX, "cmve_topk_batch_workspace: k must be in [1, %d]", BT_KMAX);
+  const BatchWs w = batch_ws_layout(std::max<int64_t>(q->n, 1), std::max<int64_t>(q->n_pad, 256), g->n, g->n_pad, k);
+  *n_floats = w.total;
+  if (sample_rows) *sample_rows = w.ns;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
+                               float* ws, int64_t ws_floats, int32_t* out_idx, double* out_score,
+                               int32_t* unresolved) {
+  CMVE_REQUIRE(h && q && g && ws && out_idx && out_score && unresolved, "cmve_topk_batch: NULL argument");
+  CMVE_REQUIRE(k >= 1 && k <= BT_KMAX, "cmve_topk_batch: k must be in [1, %d]", BT_KMAX);
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_topk_batch: raw rows / norms missing");
+  CMVE_REQUIRE(q->d == g->d && q->d_pad == g->d_pad && q->d_pad % 64 == 0, "cmve_topk_batch: dimension mismatch");
+  CMVE_REQUIRE(g->n < (1ll << 24), "cmve_topk_batch: gallery shard must hold < 2^24 rows");
+  CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
+               "cmve_topk_batch: unknown mode %d", mode);
+  CMVE_HIP(hipMemsetAsync(unresolved, 0, sizeof(int32_t), h->stream));
+  if (q->n == 0) return CMVE_OK;
+  hipStream_t st = h->stream;
+  if (g->n == 0) {
+    CMVE_HIP(hipMemsetAsync(out_idx, 0xff, sizeof(int32_t) * q->n * k, st));
+    return CMVE_OK;
+  }
+  const BatchWs w = batch_ws_layout(q->n, q->n_pad, g->n, g->n_pad, k);
+  CMVE_REQUIRE(ws_floats >= w.total, "cmve_topk_batch: workspace has %lld floats, needs %lld",
+               (long long)ws_floats, (long long)w.total);
+  const float* qerr = mode_err(q, mode);
+  CMVE_REQUIRE(qerr && g->err_max, "cmve_topk_batch: set has no error plane for this mode");
+  float* sc = ws + w.sc;
+  uint32_t* hist = (uint32_t*)(ws + w.hist);
+  float* tau = ws + w.tau;
+  int32_t* keepall = (int32_t*)(ws + w.keepall);
+  float* hi = ws + w.hi;
+  float* lo = ws + w.lo;
+  uint64_t* cand = (uint64_t*)(ws + w.cand);
+
+  // 1. sample scores: the first ns gallery rows (a prefix view shares every plane and err_max)
+  cmve_rows_t sv = *g;
+  sv.n = w.ns;
+  sv.n_pad = w.ns_pad;
+  int rc = cmve_sim_store(h, q, &sv, mode, 1.0f, 0.0f, sc, CMVE_F32, w.ns_pad);
+  if (rc) return rc;
+  // 2. per-query tau from the sample's histogram (K12b / K12c)
+  const int64_t nchunk = std::min<int64_t>(std::max<int64_t>(1, 1024 / q->n),
+                                           std::max<int64_t>(1, (w.ns + CHUNK_MIN - 1) / CHUNK_MIN));
+  const int64_t chunk = (((w.ns + nchunk - 1) / nchunk) + 255) & ~(int64_t)255;
+  const int64_t nch = (w.ns + chunk - 1) / chunk;
+  if (nch > 1) CMVE_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * q->n * HBINS, st));
+  hipLaunchKernelGGL(score_hist_kernel, dim3((unsigned)nch, (unsigned)q->n), dim3(1024), 0, st, sc, w.ns_pad, w.ns,
+                     chunk, hist);
+  rc = check_launch("score_hist_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(topk_thresh_kernel, dim3((unsigned)q->n), dim3(256), 0, st, hist, k, qerr, g->err_max,
+                     mode_slot(mode), g->d_pad, mode, tau, keepall);
+  rc = check_launch("topk_thresh_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(topk_batch_thr_kernel, dim3((unsigned)((q->n_pad + 255) / 256)), dim3(256), 0, st, tau, keepall,
+                     q->n, q->n_pad, hi, lo);
+  rc = check_launch("topk_batch_thr_kernel");
+  if (rc) return rc;
+  // 3. the whole gallery: every s~ >= tau -> its query tile's bucket
+  CMVE_HIP(hipMemsetAsync(cand, 0, sizeof(uint64_t) * w.nb, st));
+  rc = launch_topk_gemm(st, q, g, mode, hi, lo, cand, w.nb, w.cap_b);
+  if (rc) return rc;
+  // 4. per query: select T~_k over its entries, fp64 re-score of the 2E band, sort
+  const unsigned nblk = (unsigned)((q->n + BT_Q - 1) / BT_Q);
+#define TB(TQ, TG)                                                                                                 \
+  hipLaunchKernelGGL((topk_batch_finish_kernel<TQ, TG>), dim3(nblk), dim3(1024), 0, st,                           \
+                     (const unsigned long long*)cand, (const unsigned long long*)(cand + w.nb), w.cap_b, q->n, k,  \
+                     keepall, (const TQ*)q->raw, q->raw_ld, q->inv_norm, qerr, (const TG*)g->raw, g->raw_ld,      \
+                     g->inv_norm, g->err_max, mode_slot(mode), q->d, q->d_pad, mode, out_idx, out_score, unresolved)
+  if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) TB(float, float);
+  else if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F64) TB(float, double);
+  else if (q->raw_dtype == CMVE_F64 && g->raw_dtype == CMVE_F32) TB(double, float);
+  else TB(double, double);
+#undef TB
+  return check_launch("topk_batch_finish_kernel");
 }

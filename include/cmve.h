@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 4
+#define CMVE_ABI_VERSION 5
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -332,6 +332,26 @@ int cmve_gt_positions_from_matrix(cmve_handle_t h, const void* errors, int32_t d
 int cmve_topk_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* n_floats);
 int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
               float* scores_ws, int64_t ws_floats, int32_t* out_idx, double* out_score, int32_t* overflow);
+
+/*
+ * K13 -- exact top-k for a large query batch WITHOUT the n_q x n_g score matrix (the north
+ * star's 16,384-caption batches against a gallery shard; same contract and results as
+ * cmve_topk, LINAS-engine/inference.py:78-79 applied per caption).
+ *   1. s~ of every query against the first `sample_rows` gallery rows (written by
+ *      cmve_topk_batch_workspace): its per-query histogram gives tau_i <= T~_k(sample) - 2E
+ *      <= T~_k(gallery) - 2E;
+ *   2. one MFMA pass over the whole gallery whose epilogue emits every s~ >= tau_i;
+ *   3. per query: select T~_k among its entries, re-score the 2E band in fp64, sort
+ *      (score desc, index asc).
+ * A query whose entries exceed 512, whose band exceeds 256, or whose sample holds fewer than k
+ * finite scores is left UNRESOLVED: out_idx[i, :] = -2, and *unresolved (device int32) counts
+ * them; the caller re-runs those rows through cmve_topk (the host mirror does).  1 <= k <= 128;
+ * the gallery shard must hold < 2^24 rows.
+ */
+int cmve_topk_batch_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* sample_rows,
+                              int64_t* n_floats);
+int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
+                    float* ws, int64_t ws_floats, int32_t* out_idx, double* out_score, int32_t* unresolved);
 
 /* ---- non-cosine measures ---------------------------------
  * K10: out[i, j] = alpha * f(A_i, B_j) + beta over all pairs, fp64 accumulation.

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 4
+    assert _lib.lib.cmve_abi_version() == 5
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)
@@ -50,3 +50,18 @@ def test_gfx950_code_object_present():
     from cmve import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+def test_topk_batch_workspace_sizes_the_sample():
+    """cmve_topk_batch_workspace (host-only): the sample covers ~k * n_g / 128 gallery rows,
+    rounded up to the 256-row pad, and the workspace holds its score block."""
+    from cmve import _lib
+    q, g = _lib.Rows(), _lib.Rows()
+    q.n, q.n_pad, q.d, q.d_pad = 16384, 16384, 1024, 1024
+    g.n, g.n_pad, g.d, g.d_pad = 131072, 131072, 1024, 1024
+    ns, nf = C.c_int64(), C.c_int64()
+    assert _lib.lib.cmve_topk_batch_workspace(C.byref(q), C.byref(g), 10, C.byref(ns), C.byref(nf)) == 0
+    assert ns.value == 10240
+    assert nf.value >= 16384 * 10240
+    assert _lib.lib.cmve_topk_batch_workspace(C.byref(q), C.byref(g), 129, C.byref(ns), C.byref(nf)) < 0
+    assert b"k must be" in _lib.lib.cmve_last_error()
