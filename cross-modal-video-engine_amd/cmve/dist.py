@@ -83,9 +83,22 @@ def ranks_from(cnt: torch.Tensor, sgt: torch.Tensor, n_q: int, n_global: int) ->
     return torch.where(no_gt, torch.full_like(c, n_global + 1), c + 1)
 
 
-def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: int):
+def pad_topk(idx: torch.Tensor, scores: torch.Tensor, k: int):
+    """Pad a local [n_q, kk] top-k to k columns with empty slots (id -1, score NaN)."""
+    n_q, kk = idx.shape
+    if kk >= k:
+        return idx, scores
+    pi = torch.full((n_q, k - kk), -1, dtype=idx.dtype, device=idx.device)
+    ps = torch.full((n_q, k - kk), float("nan"), dtype=scores.dtype, device=scores.device)
+    return torch.cat([idx, pi], 1), torch.cat([scores, ps], 1)
+
+
+def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: int, to_host: bool = True):
     """Gather every shard's local top-k (global ids, fp64 scores) and keep the best k per query,
-    ordered (score desc, global id asc).  idx_global/scores: [n_q, k_local]."""
+    ordered (score desc, global id asc) -- on the device: a stable sort by id, then a stable sort by
+    descending score.  idx_global/scores: [n_q, k_local]; id -1 marks an empty slot (score ignored).
+    Returns (ids int64 [n_q, k'], scores fp64 [n_q, k']) with k' = min(k, world * k_local); slots
+    past the available entries hold -1 / NaN."""
     n_q, kk = idx_global.shape
     if world > 1:
         gi = torch.empty((world * n_q, kk), dtype=idx_global.dtype, device=idx_global.device)
@@ -94,19 +107,22 @@ def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: in
         dist.all_gather_into_tensor(gs, scores.contiguous())
         idx_global = gi.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
         scores = gs.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
-    idx_h = idx_global.cpu().numpy()
-    sc_h = scores.cpu().numpy()
-    kout = min(k, idx_h.shape[1])
-    out = np.empty((n_q, kout), np.int64)
-    out_s = np.empty((n_q, kout))
-    for i in range(n_q):
-        valid = idx_h[i] >= 0
-        order = np.lexsort((idx_h[i][valid], -sc_h[i][valid]))[:kout]
-        out[i, :order.size] = idx_h[i][valid][order]
-        out_s[i, :order.size] = sc_h[i][valid][order]
-        out[i, order.size:] = -1
-        out_s[i, order.size:] = np.nan
-    return out, out_s
+    ids = idx_global.to(torch.int64)
+    sc = scores.to(torch.float64)
+    empty = ids < 0
+    key_id = torch.where(empty, torch.full_like(ids, torch.iinfo(torch.int64).max), ids)
+    key_sc = torch.where(empty, torch.full_like(sc, -float("inf")), sc)
+    o1 = torch.argsort(key_id, dim=1, stable=True)
+    key_id, key_sc, empty = key_id.gather(1, o1), key_sc.gather(1, o1), empty.gather(1, o1)
+    o2 = torch.argsort(-key_sc, dim=1, stable=True)
+    kout = min(k, ids.shape[1])
+    o2 = o2[:, :kout]
+    out_id, out_sc, out_empty = key_id.gather(1, o2), key_sc.gather(1, o2), empty.gather(1, o2)
+    out_id = torch.where(out_empty, torch.full_like(out_id, -1), out_id)
+    out_sc = torch.where(out_empty, torch.full_like(out_sc, float("nan")), out_sc)
+    if not to_host:
+        return out_id, out_sc
+    return out_id.cpu().numpy(), out_sc.cpu().numpy()
 
 
 class ShardedGallery:
@@ -189,9 +205,10 @@ class ShardedGallery:
         q_all = self.all_gather_rows(q_local)
         q = engine.RowSet(q_all, with_lo=self.shard.has_lo, with_f16=self.shard.has_f16, device=self.device)
         kk = min(k, self.shard.n)
-        idx, sc = engine.topk(q, self.shard, kk, mode=mode)
-        idx = torch.from_numpy(np.where(idx >= 0, idx + self.offset, -1)).to(self.device)
-        sc = torch.from_numpy(sc).to(self.device)
+        idx, sc = engine.topk(q, self.shard, kk, mode=mode, to_host=False)
+        idx = idx.to(torch.int64)
+        idx = torch.where(idx >= 0, idx + self.offset, idx)
+        idx, sc = pad_topk(idx, sc, k)  # every rank contributes k columns (shards may hold fewer rows)
         return merge_topk(idx, sc, k, self.world)
 
 

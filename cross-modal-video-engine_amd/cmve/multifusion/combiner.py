@@ -109,6 +109,27 @@ class Combiner(nn.Module):
 
     @torch.no_grad()
     def combine_features(self, image_features, text_features):
+        """combiner.py:146-180 on one batch (the raw reshapes mix the whole batch)."""
+        return self._combine(image_features, text_features, None)
+
+    @torch.no_grad()
+    def combine_batches(self, image_features, text_features, batch_size: int = 32):
+        """Equal to concatenating combine_features over consecutive batches of ``batch_size`` rows
+        (validate.py:207-208's loop; the last partial batch is its own batch), bit for bit -- but the
+        full batches run as ONE pass: every GEMM / LayerNorm / pool is row-wise, and the attention's
+        batch-mixing key layout (combiner.py:164-165) is rebuilt per batch (keys of query (g, bb) at
+        rows t * B + g * batch_size + bb), so the GEMMs see M = all rows instead of one batch."""
+        ref_high, ref_mid = image_features
+        n = ref_mid.shape[0]
+        full = (n // batch_size) * batch_size
+        outs = []
+        if full:
+            outs.append(self._combine((ref_high[:full], ref_mid[:full]), text_features[:full], batch_size))
+        if full < n:
+            outs.append(self._combine((ref_high[full:], ref_mid[full:]), text_features[full:], None))
+        return torch.cat(outs) if len(outs) > 1 else outs[0]
+
+    def _combine(self, image_features, text_features, group):
         if self.training:
             raise NotImplementedError("cmve Combiner: eval-mode forward only (training is SURVEY 8f 'next')")
         ref_high, ref_mid = image_features
@@ -116,6 +137,10 @@ class Combiner(nn.Module):
         ref_mid = ref_mid.float()
         text = text_features.float().contiguous()
         b, f, l, d = ref_mid.size()
+        gs = b if group is None else int(group)
+        if b % gs:
+            raise ValueError("combine_batches: rows must be a multiple of the batch size")
+        G = b // gs
         n = b * f
         # conv1x1 over the raw reshape (b*f, -1, 4, 4) (combiner.py:159): channel c = elements c*16 .. c*16+15
         C = ref_mid[0, 0].numel() // 16
@@ -126,7 +151,10 @@ class Combiner(nn.Module):
         p_r_m = _linear(text, self.m_residual.weight, self.m_residual.bias, ACT_RELU, packed=self._p("m_residual"))
         # ResidualAttentionBlock(q = p_r_m [1,b,d], k = v = p_s_m.reshape(l*f, b, d))  combiner.py:38-43,164-165
         blk = self.self_attn_1
-        kv_in = p_s_m.reshape(l * f * b, d)                 # row t*b + bb  ==  [t, bb] of reshape(l*f, b, d)
+        # row t*b + bb == [t, bb] of reshape(l*f, b, d); with G batches of gs rows each batch's raw
+        # reshape is taken separately and interleaved: row t*b + g*gs + bb
+        kv_in = p_s_m.reshape(l * f * b, d) if G == 1 else \
+            p_s_m.reshape(G, l * f, gs, d).transpose(0, 1).reshape(l * f * b, d)
         kv_ln = _layernorm(kv_in, blk.ln_1)
         q_ln = _layernorm(p_r_m, blk.ln_1)
         W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
@@ -135,7 +163,7 @@ class Combiner(nn.Module):
         attn = torch.empty((b, d), dtype=torch.float32, device=text.device)
         check(lib.cmve_mha_1q(engine.handle(text.device), engine._ptr(q), q.stride(0), engine._ptr(kv), kv.stride(0), d,
                               b, l * f, self.nhead, d // self.nhead, engine._ptr(attn), attn.stride(0)), "cmve_mha_1q")
-        v3 = p_s_m.reshape(l * f, b, d)
+        v3 = kv_in.view(l * f, b, d)
         v_mean = temporal_pool(v3.transpose(0, 1), "mean")                    # v.mean(dim=0), strided view
         x = _linear(attn, blk.attn.out_proj.weight, blk.attn.out_proj.bias, resid=v_mean, packed=self._p("out_proj"))
         h = _linear(_layernorm(x, blk.ln_2), blk.mlp.c_fc.weight, blk.mlp.c_fc.bias, ACT_QUICKGELU,

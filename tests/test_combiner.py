@@ -49,3 +49,21 @@ def test_gpu_combiner(golden, state):
     alone = m.combine_features((torch.from_numpy(high[:7]).cuda(), torch.from_numpy(mid[:7]).cuda()),
                                torch.from_numpy(text[:7]).cuda())
     np.testing.assert_allclose(alone.cpu().numpy(), g["pred_b32_first7_alone"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_combine_batches_equals_batch_loop(state):
+    """combine_batches (all full 32-row batches in one pass, per-batch attention layout rebuilt) is
+    bit-identical to validate.py's loop of combine_features over consecutive batches of 32, the
+    last partial batch (7 rows) included; and it still mixes rows within each batch only."""
+    import torch
+    from cmve.multifusion.combiner import Combiner
+    m = Combiner(640, 2560, 5120).cuda()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()})
+    m.eval()
+    parts = [synth.combiner_inputs(32, 31 + i)[:3] for i in range(3)] + [synth.combiner_inputs(7, 40)[:3]]
+    high, mid, text = (torch.from_numpy(np.concatenate([p[j] for p in parts])).cuda() for j in range(3))
+    loop = torch.cat([m.combine_features((high[i:i + 32], mid[i:i + 32]), text[i:i + 32])
+                      for i in range(0, high.shape[0], 32)])
+    fused = m.combine_batches((high, mid), text, batch_size=32)
+    assert torch.equal(loop, fused)

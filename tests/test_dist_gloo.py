@@ -36,6 +36,9 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         rng = np.random.default_rng(11)
         gal = rng.standard_normal((n_g, d))
         gts = [list(rng.choice(n_g, size=int(rng.integers(0, 3)), replace=False)) for _ in range(n_q)]
+        used = {int(x) for g in gts for x in g}
+        zero = [j for j in range(3, n_g, 7) if j not in used]
+        gal[zero] = 0.0  # zero videos (never a GT): NaN scores, ranked last in index order
         qs = gal[[g[0] if g else 0 for g in gts]] + 0.8 * rng.standard_normal((n_q, d))
         lo, hi = D.shard_bounds(n_g, world, rank)
         # each rank contributes its query slice; all-gather restores the global order
@@ -60,6 +63,7 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         order = np.argsort(-s, axis=1, kind="stable")[:, :kk]
         idx_g = torch.from_numpy(order + lo)
         sc = torch.from_numpy(np.take_along_axis(s, order, axis=1))
+        idx_g, sc = D.pad_topk(idx_g, sc, k)
         top, _ = D.merge_topk(idx_g, sc, k, world)
         if rank == 0:
             s_full = R.exact_scores64(qs, gal)
@@ -70,7 +74,7 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_g", [301, 512])
+@pytest.mark.parametrize("n_g", [9, 301, 512])
 def test_sharded_protocol_world2(n_g):
     world, n_q, d, k = 2, 40, 24, 7
     ctx = mp.get_context("spawn")
