@@ -281,15 +281,35 @@ __device__ void select_rescore_sort(const Src& src, FinishLds& L, int64_t row, i
       if ((key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t acc = 0;
-      int b = 255;
-      for (; b > 0; --b) {
-        if (acc + L.hist[b] >= need) break;
-        acc += L.hist[b];
+    if (wave == 0) {
+      // digit holding the need-th largest key: bins from the top, 4 per lane, wave suffix sums
+      // (a serial 256-bin walk by one thread was ~7 us of dependent LDS reads per pass)
+      uint32_t hb[4], v = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v += (hb[i] = L.hist[4 * lane + i]);
+      uint32_t t = v;  // inclusive suffix sum over lanes >= lane
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_down(t, off, 64);
+        if (lane + off < 64) t += o;
       }
-      L.sh_prefix = prefix | ((uint32_t)b << shift);
-      L.sh_need = need - acc;
+      const uint32_t above = t - v;  // keys in bins above this lane's four
+      const uint32_t total = __shfl(t, 0, 64);
+      if (total < need) {  // fewer keys than needed: digit 0 (as the serial walk ends)
+        if (lane == 0) {
+          L.sh_prefix = prefix;
+          L.sh_need = need - (total - hb[0]);
+        }
+      } else if (above < need && need <= t) {
+        uint32_t acc = above;
+        int b = 3;
+        for (; b > 0; --b) {
+          if (acc + hb[b] >= need) break;
+          acc += hb[b];
+        }
+        L.sh_prefix = prefix | ((uint32_t)(4 * lane + b) << shift);
+        L.sh_need = need - acc;
+      }
     }
     __syncthreads();
     prefix = L.sh_prefix;
