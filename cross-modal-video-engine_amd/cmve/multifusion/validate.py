@@ -39,11 +39,22 @@ def element_wise_sum(image_features, text_features):
     return normalize(image_features[0])
 
 
+def _as_int64(names) -> np.ndarray:
+    """int(v) of every name (ints, numpy ints or numeric strings), vectorised when possible."""
+    a = np.asarray(names)
+    if a.dtype.kind in "iu":
+        return a.astype(np.int64, copy=False).reshape(-1)
+    try:
+        return a.astype(np.int64).reshape(-1)
+    except (TypeError, ValueError):
+        return np.asarray([int(v) for v in names], np.int64)
+
+
 def _positions(index_names: Sequence, names: Sequence) -> np.ndarray:
     """Row of each name in index_names (-1 when absent; the last row of a repeated name, as a
     {name: row} dict built in order), vectorised (30k lookups per val pass)."""
-    keys = np.asarray([int(v) for v in index_names], np.int64)
-    want = np.asarray([int(v) for v in names], np.int64)
+    keys = _as_int64(index_names)
+    want = _as_int64(names)
     if keys.size == 0:
         return np.full(want.shape, -1, np.int64)
     order = np.argsort(keys, kind="stable")

@@ -12,7 +12,7 @@
 //   G256: 2 x 4 waves, 128 x 64 per wave -> 256 x 256 block tile, 512 threads, 1 block / CU
 // The 256^2 tile doubles the FLOP per staged byte (128 vs 64 FLOP/B), which a 128^2 tile
 // cannot feed from L2 at the MFMA rate (~63 B/clk/CU needed vs ~56 available); G256 is the
-// default for bf16/fp16 problems with >= 512 tiles, G128 for split-bf16 (4 planes) and small
+// default for problems with >= 512 tiles (split-bf16 included: one bf16 GEMM over K' = 3K), G128 for small
 // problems.  K step 64; staging by global_load_lds_dwordx4 (16 B / lane, 1 KiB per wave
 // instruction) into a lane-linear LDS image, 2 stages; bank conflicts removed by an XOR
 // swizzle applied to the GLOBAL source chunk (chunk ^ (row & 7)) and the matching
@@ -42,7 +42,8 @@ struct SimArgs {
   int64_t ldk;  // d_pad
   int nq, ng;
   int nblk_m, nblk_n;
-  int nk;
+  int nk;   // K-tiles of the MFMA loop (split-bf16: 3 x nk0, see plane_of)
+  int nk0;  // K-tiles of one plane (d_pad / BK)
   int gn;  // gallery tiles per tile-order group
   // linear epilogue: v = acc + bias; act; + resid; v * bn_scale + bn_shift
   const float* bias;
@@ -178,9 +179,11 @@ struct Geo {
   static constexpr int BN = WN * TN * 16;
 };
 
-template <int MODE, int BM, int BN>
+// staged bytes per K-tile: one plane per operand; the 2-stage G128 loop stages both planes of a
+// split-bf16 operand per K-tile, the phased G256 loop walks the planes along K (plane_of)
+template <int MODE, int BM, int BN, bool PHASED>
 constexpr size_t stage_bytes() {
-  return (size_t)((MODE == CMVE_SIM_BF16X3) ? 2 : 1) * (BM + BN) * BK * 2;
+  return (size_t)((MODE == CMVE_SIM_BF16X3 && !PHASED) ? 2 : 1) * (BM + BN) * BK * 2;
 }
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
@@ -189,6 +192,18 @@ constexpr size_t stage_bytes() {
 #else
 #define CMVE_STAMP(k)
 #endif
+
+// Split-bf16 (BF16X3) in the phased G256 loop: ONE bf16 GEMM over K' = 3K whose K'-tile 3t + p
+// stages K-tile t of plane pair p = 0 (A lo, B hi), 1 (A hi, B lo), 2 (A hi, B hi) -- every
+// product of the split once (n = 3 d).  The G128 loop stages all four planes of
+// K-tile t and issues the same three pairs in the same order, so both geometries accumulate
+// every output element in the identical MFMA sequence (bit-identical results across shapes).
+__device__ __forceinline__ void plane_of(int tp, bool& a_lo, bool& b_lo, int& kt) {
+  kt = tp / 3;
+  const int p = tp - 3 * kt;
+  a_lo = p == 0;
+  b_lo = p == 1;
+}
 
 // Barrier for LDS hand-offs only: unlike __syncthreads it does not drain vmcnt, so loads issued
 // for the next tile stay in flight across the epilogue's barriers.
@@ -221,9 +236,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN>();
+  constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED>();
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  static_assert(!PHASED || MODE != CMVE_SIM_BF16X3, "the phased path stages one plane per operand");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
@@ -600,15 +614,26 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     };
     __amdgpu_buffer_rsrc_t rA = rsrc_of(a.qhi, m0, BM);
     __amdgpu_buffer_rsrc_t rB = rsrc_of(a.ghi, n0, BN);
+    // split-bf16: the lo planes too (plane_of picks per K-tile); else unused copies
+    __amdgpu_buffer_rsrc_t rAl = rA, rBl = rB;
+    if constexpr (MODE == CMVE_SIM_BF16X3) {
+      rAl = rsrc_of(a.qlo, m0, BM);
+      rBl = rsrc_of(a.glo, n0, BN);
+    }
     // piece = 8 rows x 128 B (one wave-instruction, 1 KiB): lane l -> row l>>3, LDS chunk l&7,
     // global chunk (l&7) ^ (row&7)
     const int voff = (lane >> 3) * ldk_b + (((lane & 7) ^ (lane >> 3)) << 4);
-    auto stage_op = [&](const __amdgpu_buffer_rsrc_t& r, int t, int plane_off) {
+    auto stage_op = [&](const __amdgpu_buffer_rsrc_t& rhi, int t, int plane_off) {
 #ifdef CMVE_DBG_NOLOAD  // diagnostic build only: MFMA + LDS-read ceiling (results are garbage)
       return;
 #endif
       char* dst = smem + (t & 1) * STAGE_BYTES + plane_off;
-      const int kb = t * (BK * 2);
+      bool alo = false, blo = false;
+      int kt = t;
+      if constexpr (MODE == CMVE_SIM_BF16X3) plane_of(t, alo, blo, kt);
+      const bool lo_plane = plane_off == 0 ? alo : blo;
+      const __amdgpu_buffer_rsrc_t r = !lo_plane ? rhi : (plane_off == 0 ? rAl : rBl);
+      const int kb = kt * (BK * 2);
 #pragma unroll
       for (int it = 0; it < 4; ++it) {  // 32 pieces per 256-row plane, 4 per wave
         const int piece = wave * 4 + it;
@@ -715,6 +740,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       tile_origin(next, m0n, n0n);
       rA = rsrc_of(a.qhi, m0n, BM);
       rB = rsrc_of(a.ghi, n0n, BN);
+      if constexpr (MODE == CMVE_SIM_BF16X3) {
+        rAl = rsrc_of(a.qlo, m0n, BM);
+        rBl = rsrc_of(a.glo, n0n, BN);
+      }
       prologue_loads();
       if constexpr (epi_thr(EPI)) fetch_thr(m0n, n0n, thn_hi, thn_lo);
     }
@@ -734,8 +763,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = 0; t < a.nk; ++t) {
-    if (t + 1 < a.nk) stage(t + 1, (t + 1) & 1);
+  for (int t = 0; t < a.nk0; ++t) {
+    if (t + 1 < a.nk0) stage(t + 1, (t + 1) & 1);
     const char* base = smem + (t & 1) * STAGE_BYTES;
     const char* pA = base;
     const char* pB = base + A_BYTES;
@@ -750,29 +779,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag(pA, wr * (TM * 16) + i * 16 + frow, chunk);
     }
-    if constexpr (MODE == CMVE_SIM_BF16X3) {
-      const char* pAl = base + A_BYTES + B_BYTES;
-      const char* pBl = base + 2 * A_BYTES + B_BYTES;
-      s16x8_t la[2][TM], lb[2][TN];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int chunk = ks * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) la[ks][i] = read_frag(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) lb[ks][j] = read_frag(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            acc[i][j] = mfma<MODE>(la[ks][i], fb[ks][j], acc[i][j]);
-            acc[i][j] = mfma<MODE>(fa[ks][i], lb[ks][j], acc[i][j]);
-          }
-    }
     __builtin_amdgcn_sched_barrier(0);
 #ifdef CMVE_DBG_NOMFMA
 #pragma unroll
@@ -783,6 +789,35 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[ks][j]));
     }
 #else
+    if constexpr (MODE == CMVE_SIM_BF16X3) {  // pairs (lo, hi) then (hi, lo): plane_of's order
+      const char* pAl = base + A_BYTES + B_BYTES;
+      const char* pBl = base + 2 * A_BYTES + B_BYTES;
+      s16x8_t lx[2][TM > TN ? TM : TN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) lx[ks][i] = read_frag(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(lx[ks][i], fb[ks][j], acc[i][j]);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) lx[ks][j] = read_frag(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], lx[ks][j], acc[i][j]);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -803,7 +838,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN>();  // + the static epilogue scratch (EpiLds)
+  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
   static bool attr_done = false;
   if (!attr_done) {
     CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
@@ -841,11 +876,10 @@ static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStrea
     const char* e = getenv("CMVE_SIM_GEO");
     return e ? atoi(e) : 0;
   }();
-  if constexpr (MODE != CMVE_SIM_BF16X3) {
-    if (force != 128 && nq_pad % 256 == 0 && ng_pad % 256 == 0 && (nq_pad / 256) * (ng_pad / 256) >= 512) {
+  if (force != 128 && nq_pad % 256 == 0 && ng_pad % 256 == 0 && (nq_pad / 256) * (ng_pad / 256) >= 512) {
+    if constexpr (MODE != CMVE_SIM_BF16X3)  // (split-bf16 takes the phased loop only)
       if (force == 2562) return launch_geo<MODE, EPI, 2, 4, 8, false>(a, nq_pad, ng_pad, stream);  // 2-stage BK64
-      return launch_geo<MODE, EPI, 2, 4, 8, true>(a, nq_pad, ng_pad, stream);
-    }
+    return launch_geo<MODE, EPI, 2, 4, 8, true>(a, nq_pad, ng_pad, stream);
   }
   return launch_geo<MODE, EPI, 2, 2, 4, false>(a, nq_pad, ng_pad, stream);
 }
@@ -874,7 +908,8 @@ static SimArgs make_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mod
   a.ldk = q->d_pad;
   a.nq = (int)q->n;
   a.ng = (int)g->n;
-  a.nk = (int)(q->d_pad / BK);
+  a.nk0 = (int)(q->d_pad / BK);
+  a.nk = mode == CMVE_SIM_BF16X3 ? 3 * a.nk0 : a.nk0;
   return a;
 }
 

@@ -51,8 +51,9 @@ def main():
     out["gallery_prep_ms"] = (time.perf_counter() - t0) * 1e3
     high = index[ref]
 
-    # warm-up (packs the weights once)
+    # warm-up (packs the weights once; first launches of every kernel and tile shape)
     m.combine_batches((high[:64], mid[:64]), text[:64])
+    m.combine_batches((high[:a.chunk], mid[:a.chunk]), text[:a.chunk])
     torch.cuda.synchronize()
     # (a) the reference's loop structure: one combine_features call per batch of 32
     nl = min(a.loop_q, a.nq) // 32 * 32
@@ -80,10 +81,15 @@ def main():
     out["combine_batches"]["identical_to_loop"] = bool(same)
     # (c) exact target ranks with reference removal (validate.py:71-138)
     names = list(range(a.nv))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ranks = V.cirr_target_ranks(pred, pooled, names, ref.tolist(), tgt.tolist())
-    dt_r = time.perf_counter() - t0
+    refs, tgts = ref.tolist(), tgt.tolist()
+    V.cirr_target_ranks(pred[:512], pooled, names, refs[:512], tgts[:512])  # warm-up (first launches)
+    dts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ranks = V.cirr_target_ranks(pred, pooled, names, refs, tgts)
+        dts.append(time.perf_counter() - t0)
+    dt_r = float(np.median(dts))
     found = ranks > 0
     out["ranking"] = {"ms": dt_r * 1e3, "pairs_per_s": a.nq * a.nv / dt_r,
                       "recall_at_1_5_10_50": [float(100.0 * np.count_nonzero(found & (ranks <= k)) / a.nq)
