@@ -80,26 +80,40 @@ def msrvtt1ka(steps=20):
     vt = torch.from_numpy(v).cuda()
     ct = torch.from_numpy(c).cuda()
 
+    # the evaluation as the reference's validation loop re-runs it (validate.py:61-74): resident
+    # buffers, the evaluation enqueued as one sequence (pack both sets, GT thresholds, rank GEMM, fix-up)
+    sess = engine.RankSession(len(cid), len(vid), v.shape[1], row_gts=t2v_lists, col_gts=v2t_gt,
+                              dtype=vt.dtype, device=vt.device)
+
     def step():
-        caps = engine.RowSet(ct, with_lo=False)
-        vids = engine.RowSet(vt, with_lo=False)
-        return engine.gt_rank_counts(caps, vids, row_gts=t2v_lists, col_gts=v2t_gt)
+        return sess.run(ct, vt)
 
     for _ in range(3):
-        t2v, v2t, _ = step()
+        t2v, v2t = step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        t2v, v2t, _ = step()
+        t2v, v2t = step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    # the same evaluation without the session (fresh packing, workspace and launches per call)
+    engine.gt_rank_counts(engine.RowSet(ct, with_lo=False), engine.RowSet(vt, with_lo=False),
+                          row_gts=t2v_lists, col_gts=v2t_gt)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(5):
+        e_t, e_v, _ = engine.gt_rank_counts(engine.RowSet(ct, with_lo=False), engine.RowSet(vt, with_lo=False),
+                                            row_gts=t2v_lists, col_gts=v2t_gt)
+    dt_eager = (time.perf_counter() - t1) / 5
     t2v_m = M.metrics_from_ranks(t2v)
     v2t_m = M.metrics_from_ranks(v2t)
-    parity = bool(np.array_equal(t2v, gold["t2v_ranks"]) and np.array_equal(v2t, gold["v2t_ranks"]))
-    return {"pairs_per_s": 1000 * 1000 / dt, "ms_per_eval": dt * 1e3,
+    parity = bool(np.array_equal(t2v, gold["t2v_ranks"]) and np.array_equal(v2t, gold["v2t_ranks"])
+                  and np.array_equal(e_t, t2v) and np.array_equal(e_v, v2t))
+    return {"pairs_per_s": 1000 * 1000 / dt, "ms_per_eval": dt * 1e3, "ms_per_eval_eager": dt_eager * 1e3,
             "t2v_r1_r5_r10": [round(x, 3) for x in t2v_m[:3]], "v2t_r1_r5_r10": [round(x, 3) for x in v2t_m[:3]],
             "ref_t2v_r1_r5_r10": [float(x) for x in gold["t2v"][:3]], "parity_exact": parity,
-            "note": "includes gallery+query packing, GT scoring, both directions, D2H of ranks"}
+            "note": "RankSession (resident buffers): device copy-in, packing of both sets, GT scoring, both directions, "
+                    "D2H of ranks; eager = the same through fresh RowSets / gt_rank_counts"}
 
 
 def inference_leg(n_gallery=1048576, d=1024, k=10, reps=20, cpu_rows=262144):

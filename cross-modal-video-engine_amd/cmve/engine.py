@@ -309,6 +309,124 @@ def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int =
     return out_r, out_c, ncand
 
 
+class RankSession:
+    """Resident exact GT-rank evaluation of a fixed problem (the reference re-runs
+    ``encode_* -> cal_error -> cal_perf`` on new embeddings of the same sets every validation,
+    ``LINAS-engine/validate.py:61-74``): raw / packed buffers of both sets, the GT lists, thresholds,
+    counts and the undecided-pair list are allocated once, and one evaluation -- pack both sets,
+    GT scores and thresholds of both directions, the fused rank GEMM, the fp64 fix-up, ranks --
+    is enqueued on a stream of its own.  ``run(captions, videos)`` copies the new embeddings in and
+    returns (t2v ranks, v2t ranks) as ``gt_rank_counts`` does, bit for bit.  An undecided-pair
+    overflow (checked after every run) grows the list and redoes the run.
+    graph=True captures the evaluation into one hipGraph.  Its replays raced with a device-to-device
+    input copy ordered only by a stream wait (garbage pair counts after a few replays on the MI355X
+    box), so a replay first synchronises the device; measured 0.22 ms per C1 evaluation against
+    0.19 ms for the eager enqueue, hence graph=False by default."""
+
+    def __init__(self, n_q: int, n_g: int, d: int, row_gts=None, col_gts=None, dtype=torch.float32,
+                 mode: int = _lib.SIM_F16, eps: float = 0.0, device: Optional[torch.device] = None,
+                 graph: bool = False):
+        if row_gts is None and col_gts is None:
+            raise ValueError("RankSession: need row_gts and/or col_gts")
+        self.device = device or default_device()
+        dev = self.device
+        self.mode, self.graph = mode, graph
+        self.q = RowSet(torch.zeros((n_q, d), dtype=dtype, device=dev), eps=eps, with_lo=(mode == _lib.SIM_BF16X3),
+                        with_f16=(mode == _lib.SIM_F16), device=dev)
+        self.g = RowSet(torch.zeros((n_g, d), dtype=dtype, device=dev), eps=eps, with_lo=(mode == _lib.SIM_BF16X3),
+                        with_f16=(mode == _lib.SIM_F16), device=dev)
+        self.row = self.col = None
+        if row_gts is not None:
+            off, idx = csr(row_gts, dev)
+            self.row = (off, idx) + tuple(torch.empty(self.q.n_pad, dtype=t, device=dev)
+                                          for t in (torch.float64, torch.float32, torch.float32))
+            self.row_cnt = torch.zeros(self.q.n_pad, dtype=torch.int32, device=dev)
+            self.row_empty = torch.from_numpy(np.fromiter((len(l) == 0 for l in row_gts), bool,
+                                                          count=len(row_gts))).to(dev)
+        if col_gts is not None:
+            off, idx = csr(col_gts, dev)
+            self.col = (off, idx) + tuple(torch.empty(self.g.n_pad, dtype=t, device=dev)
+                                          for t in (torch.float64, torch.float32, torch.float32))
+            self.col_cnt = torch.zeros(self.g.n_pad, dtype=torch.int32, device=dev)
+            self.col_empty = torch.from_numpy(np.fromiter((len(l) == 0 for l in col_gts), bool,
+                                                          count=len(col_gts))).to(dev)
+        self.ws = RankWorkspace(dev, cap=max(1 << 16, 64 * (n_q + n_g)))
+        self.out = torch.zeros(n_q + n_g + 1, dtype=torch.int64, device=dev)  # t2v | v2t | pair count
+        self.host = torch.zeros(n_q + n_g + 1, dtype=torch.int64).pin_memory()
+        self._graph = None
+        self._stream = torch.cuda.Stream(dev)
+        self._warm = 0
+
+    def _enqueue(self):
+        h = handle(self.device)
+        q, g, mode = self.q, self.g, self.mode
+        check(lib.cmve_pack_rows(h, C.byref(q.desc)), "cmve_pack_rows")
+        check(lib.cmve_pack_rows(h, C.byref(g.desc)), "cmve_pack_rows")
+        dirs = 0
+        for d_bit, a, b, t in ((_lib.DIR_ROW, q, g, self.row), (_lib.DIR_COL, g, q, self.col)):
+            if t is not None:
+                dirs |= d_bit
+                check(lib.cmve_gt_thresholds(h, C.byref(a.desc), C.byref(b.desc), mode, _ptr(t[0]), _ptr(t[1]),
+                                             _ptr(t[2]), _ptr(t[3]), _ptr(t[4])), "cmve_gt_thresholds")
+        r = self.row[2:] if self.row is not None else (None, None, None)
+        c = self.col[2:] if self.col is not None else (None, None, None)
+        rc = self.row_cnt if self.row is not None else None
+        cc = self.col_cnt if self.col is not None else None
+        self.ws.chunks = 1
+        check(lib.cmve_rank_mfma(h, C.byref(q.desc), C.byref(g.desc), mode, dirs, _ptr(r[1]), _ptr(r[2]),
+                                 _ptr(c[1]), _ptr(c[2]), _ptr(rc), _ptr(cc), _ptr(self.ws.cand), self.ws.cap,
+                                 _ptr(self.ws.count)), "cmve_rank_mfma")
+        check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(rc),
+                                  _ptr(cc), _ptr(self.ws.cand), self.ws.cap, _ptr(self.ws.count)), "cmve_rank_fixup")
+        nq, ng = q.n, g.n
+        if self.row is not None:
+            v = self.row_cnt[:nq].to(torch.int64) + 1
+            self.out[:nq].copy_(torch.where(self.row_empty, torch.full_like(v, ng + 1), v))
+        if self.col is not None:
+            v = self.col_cnt[:ng].to(torch.int64) + 1
+            self.out[nq:nq + ng].copy_(torch.where(self.col_empty, torch.full_like(v, nq + 1), v))
+        self.out[nq + ng:].copy_(self.ws.count[:1])
+
+    def run(self, captions, videos):
+        """Exact 1-based (t2v, v2t) ranks of new caption / video embeddings (numpy or torch)."""
+        for dst, src in ((self.q.raw, captions), (self.g.raw, videos)):
+            src_t = src if torch.is_tensor(src) else torch.from_numpy(np.ascontiguousarray(src))
+            if tuple(src_t.shape) != tuple(dst.shape):
+                raise ValueError(f"RankSession.run: expected {tuple(dst.shape)}, got {tuple(src_t.shape)}")
+            dst.copy_(src_t, non_blocking=True)
+        cur = torch.cuda.current_stream(self.device)
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            if not self.graph:
+                self._enqueue()
+            elif self._graph is None and self._warm < 2:  # eager warm-up on the capture stream
+                self._enqueue()
+                self._warm += 1
+            else:
+                if self._graph is None:
+                    self._graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._graph, stream=self._stream):
+                        self._enqueue()
+                torch.cuda.synchronize(self.device)  # see the class note
+                self._graph.replay()
+            self.host.copy_(self.out, non_blocking=True)
+        cur.wait_stream(self._stream)
+        self._stream.synchronize()
+        nq, ng = self.q.n, self.g.n
+        npairs = int(self.host[nq + ng])
+        if npairs > self.ws.cap:  # undecided pairs overflowed: grow, re-capture, redo
+            if npairs > 2 * (nq * ng + 1024 * self.g.n_pad):
+                raise _lib.CmveError(f"RankSession: impossible undecided-pair count {npairs} (cap {self.ws.cap}, "
+                                     f"device count {self.ws.count[:2].tolist()}, graph {self._graph is not None})")
+            self.ws.grow(npairs)
+            self._graph, self._warm = None, 0
+            return self.run(captions, videos)
+        h = self.host.numpy()
+        t2v = h[:nq].copy() if self.row is not None else None
+        v2t = h[nq:nq + ng].copy() if self.col is not None else None
+        return t2v, v2t
+
+
 def rank_from_matrix(errors, gts, transposed: bool = False, device=None) -> np.ndarray:
     """1-based GT ranks from a materialised error matrix (lower = better), on device."""
     device = device or default_device()

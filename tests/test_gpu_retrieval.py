@@ -352,3 +352,32 @@ def test_unpadded_fast_epilogue_each_direction(torch_cuda, dirs, nq, ng):
         assert np.array_equal(r, R.rank_counts(s, row_gts))
     if col_gts is not None:
         assert np.array_equal(c, R.rank_counts(s.T, col_gts))
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_rank_session_replays_match(golden, torch_cuda, graph):
+    """RankSession (resident buffers, one hipGraph per evaluation): C1 ranks equal the golden ranks
+    on every replay, new embeddings give the ranks gt_rank_counts computes for them, and an
+    undecided-pair overflow grows the list and re-captures without changing the result."""
+    import torch
+    from cmve import engine
+    g = golden("retrieval_c1")
+    v, c, vid, cid = _c1()
+    v2t_gt, t2v_gt = R.get_gt(vid, cid)
+    rows = [t2v_gt[i] for i in range(len(cid))]
+    sess = engine.RankSession(len(cid), len(vid), v.shape[1], row_gts=rows, col_gts=v2t_gt,
+                              dtype=torch.float64 if v.dtype == np.float64 else torch.float32, graph=graph)
+    for _ in range(4):  # warm-up, warm-up, capture + replay, replay
+        t2v, v2t = sess.run(c, v)
+        assert np.array_equal(t2v, g["t2v_ranks"]) and np.array_equal(v2t, g["v2t_ranks"])
+    rng = np.random.default_rng(8)
+    c2 = (c + 0.5 * rng.standard_normal(c.shape)).astype(c.dtype)
+    t2v2, v2t2 = sess.run(c2, v)
+    e_t, e_v, _ = engine.gt_rank_counts(engine.RowSet(c2, with_lo=False), engine.RowSet(v, with_lo=False),
+                                        row_gts=rows, col_gts=v2t_gt)
+    assert np.array_equal(t2v2, e_t) and np.array_equal(v2t2, e_v)
+    sess.ws = engine.RankWorkspace(sess.device, cap=8)
+    sess._graph, sess._warm = None, 2  # capture straight away with the tiny list
+    t2v3, v2t3 = sess.run(c, v)
+    assert sess.ws.cap > 8
+    assert np.array_equal(t2v3, g["t2v_ranks"]) and np.array_equal(v2t3, g["v2t_ranks"])

@@ -49,3 +49,15 @@ def test_element_wise_sum_ignores_text():
     out = element_wise_sum((x,), torch.randn(5, 640, device="cuda"))
     np.testing.assert_allclose(out.cpu().numpy(), torch.nn.functional.normalize(x, dim=-1).cpu().numpy(),
                                rtol=0, atol=1e-6)
+
+
+def test_positions_lookup_matches_dict():
+    """CIRR name -> gallery row lookup (vectorised): the last row of a repeated name, as the
+    reference's {name: i} dict; absent names -1; numeric strings parsed like int(v)."""
+    from cmve.multifusion.validate import _positions
+    index = [5, 3, 9, 3, 7]
+    table = {n: i for i, n in enumerate(index)}
+    want = [3, 9, 4, 5, 7, 100]
+    assert list(_positions(index, want)) == [table.get(n, -1) for n in want]
+    assert list(_positions([str(v) for v in index], [str(v) for v in want])) == [table.get(n, -1) for n in want]
+    assert list(_positions([], [1, 2])) == [-1, -1]
