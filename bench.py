@@ -50,6 +50,11 @@ def parse():
     p.add_argument("--chunks", type=int, default=1,
                    help="gallery pieces per shard: each piece's fp64 fix-up overlaps the next piece's MFMA pass")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_traffic.json"))
+    p.add_argument("--topk-leg", action="store_true",
+                   help="run the sharded exact top-k leg at any N (by default only at N=1, with the extras)")
+    p.add_argument("--rehearse-gloo", action="store_true",
+                   help="N>1 rehearsal on a 1-GPU box: gloo instead of RCCL, ranks share the visible GPUs "
+                        "(exercises every collective of the sharded path; not a measurement)")
     return p.parse_args()
 
 
@@ -57,9 +62,14 @@ def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_gloo:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
 
 
@@ -294,6 +304,9 @@ def main():
     rank_ms = float(np.mean([e[0].elapsed_time(e[2]) for e in ev]))
     ncand = scorer.ws.ncand()
 
+    topk_out = None
+    if args.topk_leg or (world == 1 and not args.no_extras):  # collective at N > 1: every rank runs it
+        topk_out = sharded_topk_leg(scorer, q_local, nq, n_global)
     if rank == 0:
         ms = dt / args.steps * 1e3
         value = nq * n_global * args.steps / dt
@@ -314,8 +327,8 @@ def main():
             "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16",
             "data": "synthetic (torch.randn gallery shards, queries = GT video + sigma*noise; no dataset offline)",
-            "config": {"workload": "gallery-shard retrieval scoring: 16,384 text queries x (131,072 videos per GPU) "
-                                   "x 1024-d, t2v GT rank -> R@1/5/10 (fused fp16 MFMA rank count + fp64 fix-up)",
+            "config": {"workload": f"gallery-shard retrieval scoring: {nq:,} text queries x ({shard:,} videos per "
+                                   f"GPU) x {d}-d, t2v GT rank -> R@1/5/10 (fused fp16 MFMA rank count + fp64 fix-up)",
                        "queries_per_step": nq, "gallery_per_gpu": shard, "gallery_total": n_global, "dim": d,
                        "sigma": args.sigma, "parallelism": f"gallery-shard x{world} (RCCL all-gather Q, "
                                                             f"all-reduce MAX gt / SUM counts)"},
@@ -327,8 +340,9 @@ def main():
             "rank_count": {"ms": rank_ms, "chunks": chunks, "fixup_ms": fix_ms, "candidates_per_step": ncand,
                            "note": "MFMA passes + fp64 fix-ups of one step (fix-ups overlapped when chunks > 1)"},
         }
+        if topk_out is not None:
+            out["sharded_topk"] = topk_out
         if world == 1 and not args.no_extras:
-            out["sharded_topk"] = sharded_topk_leg(scorer, q_local, nq, n_global)
             out["msrvtt1kA"] = msrvtt1ka()
             out["inference_topk"] = inference_leg()
             if not args.no_cpu_baseline:
