@@ -14,7 +14,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # repo root (tests/tools/..)
 for p in (os.path.join(ROOT, "cross-modal-video-engine_amd"), ROOT):
     sys.path.insert(0, p)
 import numpy as np  # noqa: E402
