@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--nq", type=int, default=16384, help="queries per step (whole job)")
     p.add_argument("--dim", type=int, default=1024)
     p.add_argument("--sigma", type=float, default=10.0)
-    p.add_argument("--cpu-sample-queries", type=int, default=3072)
+    p.add_argument("--cpu-sample-queries", type=int, default=6144, help="CPU-baseline sample (~10-15 s of host work)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="skip the 1kA and CPU legs (profiling runs)")
     p.add_argument("--chunks", type=int, default=1,
