@@ -454,7 +454,7 @@ def topk_workspace_floats(q: RowSet, g: RowSet, k: int) -> int:
 
 
 TOPK_BATCH_MIN_Q = 512   # below this the dense score block is small: cmve_topk
-TOPK_BATCH_MAX_K = 128
+TOPK_BATCH_MAX_K = 32     # cmve_topk_batch's limit (its sample is ~k/128 of the gallery)
 
 
 def topk_batch_plan(q: RowSet, g: RowSet, k: int):

@@ -469,7 +469,7 @@ static int launch_gemv(const cmve_rows_t* q, const cmve_rows_t* g, float* ws, hi
 constexpr int BT_Q = 16;       // queries per finish block (one wave each)
 constexpr int BT_LCAP = 512;   // entries kept per query (more: the row is left to the dense path)
 constexpr int BT_BAND = 256;   // band entries re-scored per query
-constexpr int BT_KMAX = 128;
+constexpr int BT_KMAX = 32;    // k * n_g / BT_TARGET sample rows must stay <= n_g / 4 to pay off
 constexpr int BT_TARGET = 128; // expected entries per query the sample size is chosen for
 
 __global__ __launch_bounds__(256) void topk_batch_thr_kernel(const float* __restrict__ tau,

@@ -345,7 +345,8 @@ int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32
  *      (score desc, index asc).
  * A query whose entries exceed 512, whose band exceeds 256, or whose sample holds fewer than k
  * finite scores is left UNRESOLVED: out_idx[i, :] = -2, and *unresolved (device int32) counts
- * them; the caller re-runs those rows through cmve_topk (the host mirror does).  1 <= k <= 128;
+ * them; the caller re-runs those rows through cmve_topk (the host mirror does).  1 <= k <= 32
+ * (the sample is ~k/128 of the gallery; beyond a quarter the dense path is cheaper);
  * the gallery shard must hold < 2^24 rows.
  */
 int cmve_topk_batch_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* sample_rows,

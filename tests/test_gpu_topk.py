@@ -204,3 +204,23 @@ def test_topk_batch_bench_shape(torch_cuda):
     rows = np.arange(0, 4096, 4096 // 48)
     s = R.exact_scores64(qs[rows].cpu().numpy(), gal.cpu().numpy())
     _check(idx.cpu().numpy()[rows], sc.cpu().numpy()[rows], s, 10)
+
+
+@pytest.mark.parametrize("nq,ng,d,k,qdt,gdt", [(517, 70001, 200, 1, np.float64, np.float32),
+                                               (530, 140000, 96, 32, np.float32, np.float64),
+                                               (1040, 9000, 1024, 17, np.float32, np.float32)])
+def test_topk_batch_edge_shapes(torch_cuda, nq, ng, d, k, qdt, gdt):
+    """Ragged query counts (not a multiple of the 16-query finish block), unpadded gallery sizes,
+    k = 1 and k = 32 (the batch path's limit), mixed f32 / f64 raw rows: ids exact vs fp64."""
+    from cmve import engine
+    rng = np.random.default_rng(nq + k)
+    gal = rng.standard_normal((ng, d)).astype(gdt)
+    qs = (gal[rng.integers(0, ng, nq)] + 3.0 * rng.standard_normal((nq, d))).astype(qdt)
+    q = engine.RowSet(qs, with_lo=True)
+    g = engine.RowSet(gal, with_lo=True)
+    ok, ns, _ = engine.topk_batch_plan(q, g, k)
+    assert ok and ns <= ng // 4
+    idx, sc = engine.topk(q, g, k)
+    rows = np.arange(nq) if nq * ng <= 40_000_000 else np.linspace(0, nq - 1, 64).astype(int)
+    s = R.exact_scores64(qs[rows], gal)
+    _check(idx[rows], sc[rows], s, k)
