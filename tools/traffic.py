@@ -57,6 +57,17 @@ def main(outdir, tag):
         clk = last["GRBM_GUI_ACTIVE"] / 8 / last["dur"]
         out["effective_clock_ghz"] = clk / 1e9
         out["mfma_busy_frac"] = last["SQ_VALU_MFMA_BUSY_CYCLES"] / (clk * last["dur"] * 256 * 4)
+    # per-launch durations of the same kernel in the trace pass: the bench's timed launches are the
+    # last `steps` ones (the earlier ones are the workspace-sizing call and the warm-up steps)
+    tr = [r for r in rows(os.path.join(outdir, "trace", "**", "*kernel_trace.csv"))
+          if "sim_kernel<2, 1" in r.get("Kernel_Name", "")]
+    if tr:
+        tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in tr]
+        steps = int(os.environ.get("TRACE_TIMED_STEPS", "10"))
+        out["trace_launches"] = len(ms)
+        out["trace_avg_ms_all"] = sum(ms) / len(ms)
+        out["trace_avg_ms_timed"] = sum(ms[-steps:]) / len(ms[-steps:])
     out.update({"shard": 131072, "nq": 16384, "dim": 1024, "chunks": 1,
                 "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"})
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
