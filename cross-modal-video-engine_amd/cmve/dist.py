@@ -100,6 +100,11 @@ def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: in
     Returns (ids int64 [n_q, k'], scores fp64 [n_q, k']) with k' = min(k, world * k_local); slots
     past the available entries hold -1 / NaN."""
     n_q, kk = idx_global.shape
+    if world == 1:  # one shard: its top-k is already in (score desc, id asc) order
+        ids = idx_global.to(torch.int64)[:, :k]
+        sc = scores.to(torch.float64)[:, :k]
+        sc = torch.where(ids < 0, torch.full_like(sc, float("nan")), sc)
+        return (ids, sc) if not to_host else (ids.cpu().numpy(), sc.cpu().numpy())
     if world > 1:
         gi = torch.empty((world * n_q, kk), dtype=idx_global.dtype, device=idx_global.device)
         gs = torch.empty((world * n_q, kk), dtype=scores.dtype, device=scores.device)

@@ -89,3 +89,18 @@ def test_sharded_protocol_world2(n_g):
         assert p.exitcode == 0
     ranks_ok, top_ok = result_q.get()
     assert ranks_ok and top_ok
+
+
+def test_merge_topk_single_shard_is_identity():
+    """world 1: the shard's own top-k (already score desc, id asc) comes back unchanged; padded
+    empty slots read -1 / NaN."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "cross-modal-video-engine_amd"))
+    from cmve import dist as D
+    idx = torch.tensor([[5, 2, 9], [1, 0, 3]])
+    sc = torch.tensor([[0.9, 0.5, -float("inf")], [0.7, 0.7, 0.1]], dtype=torch.float64)
+    idx, sc = D.pad_topk(idx, sc, 4)
+    top, s = D.merge_topk(idx, sc, 4, 1)
+    assert top.tolist() == [[5, 2, 9, -1], [1, 0, 3, -1]]
+    assert np.isnan(s[:, 3]).all() and s[0, 2] == -np.inf
