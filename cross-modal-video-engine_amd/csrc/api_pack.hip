@@ -296,6 +296,10 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
 #undef PACK
   int st = check_launch("pack_rows");
   if (st) return st;
+  if (r->flags & CMVE_PACK_RAW) {  // GEMM operands of cmve_linear / cmve_sim_store: no score bound
+    CMVE_HIP(hipMemsetD32Async((hipDeviceptr_t)r->err_max, 0x7f800000u, 3, h->stream));  // +inf
+    return CMVE_OK;
+  }
   hipLaunchKernelGGL(err_max_kernel, dim3(1), dim3(1024), 0, h->stream, r->err_hi, r->err_hilo, r->err_h16, r->n,
                      r->err_max);
   return check_launch("pack_rows/err_max");

@@ -19,6 +19,34 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const float* xr = x + row * ldx;
+  if (d <= 1024) {  // the row read once into registers (16 per lane); same per-lane order as below
+    float v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = (lane + 64 * m < d) ? xr[lane + 64 * m] : 0.f;
+    double s = 0.0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (lane + 64 * m < d) s += (double)v[m];
+    const double mean = wave_sum(s) / (double)d;
+    double q = 0.0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+      if (lane + 64 * m < d) {
+        const double c = (double)v[m] - mean;
+        q = fma(c, c, q);
+      }
+    const double rstd = 1.0 / sqrt(wave_sum(q) / (double)d + eps);
+    float* yr = y + row * ldy;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int64_t k = lane + 64 * m;
+      if (k < d) {
+        const double c = ((double)v[m] - mean) * rstd;
+        yr[k] = (float)(c * (double)(gamma ? gamma[k] : 1.f) + (double)(beta ? beta[k] : 0.f));
+      }
+    }
+    return;
+  }
   double s = 0.0;
   for (int64_t k = lane; k < d; k += 64) s += (double)xr[k];
   const double mean = wave_sum(s) / (double)d;

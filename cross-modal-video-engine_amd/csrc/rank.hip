@@ -351,6 +351,7 @@ extern "C" int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a, const c
                                   float* thr_lo) {
   CMVE_REQUIRE(h && a && b, "cmve_gt_thresholds: NULL argument");
   CMVE_REQUIRE(a->d == b->d && a->d_pad == b->d_pad, "cmve_gt_thresholds: dimension mismatch");
+  CMVE_REQUIRE(!((a->flags | b->flags) & CMVE_PACK_RAW), "cmve_gt_thresholds: sets packed CMVE_PACK_RAW have no score bound");
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
                "cmve_gt_thresholds: unknown mode");
   CMVE_REQUIRE(off && sgt && thr_hi && thr_lo, "cmve_gt_thresholds: NULL output");
@@ -429,6 +430,7 @@ extern "C" int cmve_rank_thresholds(cmve_handle_t h, const cmve_rows_t* a, const
                                     const double* sgt, float* thr_hi, float* thr_lo) {
   CMVE_REQUIRE(h && a && b && sgt && thr_hi && thr_lo, "cmve_rank_thresholds: NULL argument");
   CMVE_REQUIRE(a->d_pad == b->d_pad, "cmve_rank_thresholds: dimension mismatch");
+  CMVE_REQUIRE(!((a->flags | b->flags) & CMVE_PACK_RAW), "cmve_rank_thresholds: sets packed CMVE_PACK_RAW have no score bound");
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
                "cmve_rank_thresholds: unknown mode");
   const float* aerr = mode_err(a, mode);

@@ -969,6 +969,7 @@ static int rank_args(const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, i
   if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_hi && row_lo && row_cnt, "%s: row arrays missing", fn);
   if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_hi && col_lo && col_cnt, "%s: col arrays missing", fn);
   CMVE_REQUIRE(cand && cand_count && cand_cap >= 0, "%s: candidate buffer missing", fn);
+  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "%s: sets packed CMVE_PACK_RAW have no score bound", fn);
   a = make_args(q, g, mode);
   if (dirs & CMVE_DIR_ROW) {
     a.row_hi = row_hi;

@@ -659,6 +659,7 @@ extern "C" int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_
   CMVE_REQUIRE(k >= 1, "cmve_topk: k must be >= 1");
   CMVE_REQUIRE(k <= TOPK_CAP / 2, "cmve_topk: k must be <= %d", TOPK_CAP / 2);
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_topk: raw rows / norms missing");
+  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "cmve_topk: sets packed CMVE_PACK_RAW have no score bound");
   CMVE_REQUIRE(q->d == g->d && q->d_pad == g->d_pad && q->d_pad % 64 == 0, "cmve_topk: dimension mismatch");
   CMVE_REQUIRE(g->n < (1ll << 31), "cmve_topk: gallery too large for int32 indices");
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16, "cmve_topk: unknown mode %d",
@@ -754,6 +755,7 @@ extern "C" int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve
   CMVE_REQUIRE(h && q && g && ws && out_idx && out_score && unresolved, "cmve_topk_batch: NULL argument");
   CMVE_REQUIRE(k >= 1 && k <= BT_KMAX, "cmve_topk_batch: k must be in [1, %d]", BT_KMAX);
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_topk_batch: raw rows / norms missing");
+  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "cmve_topk_batch: sets packed CMVE_PACK_RAW have no score bound");
   CMVE_REQUIRE(q->d == g->d && q->d_pad == g->d_pad && q->d_pad % 64 == 0, "cmve_topk_batch: dimension mismatch");
   CMVE_REQUIRE(g->n < (1ll << 24), "cmve_topk_batch: gallery shard must hold < 2^24 rows");
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,

@@ -381,3 +381,19 @@ def test_rank_session_replays_match(golden, torch_cuda, graph):
     t2v3, v2t3 = sess.run(c, v)
     assert sess.ws.cap > 8
     assert np.array_equal(t2v3, g["t2v_ranks"]) and np.array_equal(v2t3, g["v2t_ranks"])
+
+
+def test_raw_packed_sets_rejected_by_rank_and_topk(torch_cuda):
+    """Sets packed CMVE_PACK_RAW (GEMM operands: no normalisation, no score-error bound) cannot
+    be ranked: the rank / threshold / top-k entry points refuse them instead of using a bound
+    that does not exist."""
+    from cmve import engine, _lib
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((300, 64)).astype(np.float32)
+    raw = engine.RowSet(x, with_lo=True, raw_rows=True)
+    unit = engine.RowSet(x, with_lo=True)
+    assert np.isinf(raw.err_max.cpu().numpy()).all()
+    with pytest.raises(_lib.CmveError, match="PACK_RAW"):
+        engine.gt_rank_counts(raw, unit, row_gts=[[0]] * 300)
+    with pytest.raises(_lib.CmveError, match="PACK_RAW"):
+        engine.topk(unit, raw, 5)
