@@ -32,7 +32,6 @@ constexpr int BK = 64;
 constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2, EPI_TOPK = 3;
 // epilogues that count / emit against per-row and per-column thresholds
 constexpr bool epi_thr(int e) { return e == EPI_RANK || e == EPI_TOPK; }
-constexpr int CAND_LDS = 1024;  // per-block undecided-pair buffer (one global atomic per block)
 
 struct SimArgs {
   const uint16_t* qhi;
@@ -217,17 +216,11 @@ template <int BM, int BN, bool RANK>
 struct EpiLds {
   int rc[BM];
   int cc[BN];
-  unsigned long long cand[CAND_LDS];
-  unsigned ncand[2];
-  unsigned long long cand_base;
   float thr[2 * (BM + BN)];  // [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
 };
 template <int BM, int BN>
 struct EpiLds<BM, BN, false> {
   int rc[1], cc[1];
-  unsigned long long cand[1];
-  unsigned ncand[2];
-  unsigned long long cand_base;
   float thr[1];
 };
 
@@ -264,9 +257,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   __shared__ EpiLds<BM, BN, epi_thr(EPI)> epi;
   int* lds_rc = epi.rc;
   int* lds_cc = epi.cc;
-  unsigned long long* lds_cand = epi.cand;
-  unsigned* lds_ncand = epi.ncand;
-  unsigned long long* lds_cand_base = &epi.cand_base;
   float* lds_thr = epi.thr;
   float thr_hi_v = __builtin_nanf(""), thr_lo_v = __builtin_nanf("");
   // a tile's thresholds are fetched when its loads are issued and published to LDS in its
@@ -286,7 +276,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   if constexpr (epi_thr(EPI)) {
     static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
-    if (tid == 0) *lds_ncand = 0u;
     fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
   }
 
@@ -502,11 +491,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const uint32_t c = (cc_pack >> (8 * j)) & 0xffu;
-          if (c) atomicAdd(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
+          if (c) lds_add_u32_async(&lds_cc[wc * (TN * 16) + j * 16 + lane], (int)c);
         }
       }
       CMVE_STAMP(5);
-      // emission: wave-inclusive scan of the per-lane counts, one LDS atomic per wave
+      // emission: exclusive prefix of the per-lane counts, ONE returning global atomic per wave on
+      // the tile's bucket counter, issued before the count flush so its latency hides behind the
+      // barrier and the flush (a block-wide LDS staging buffer + one atomic per block cost two
+      // extra barriers with that atomic's round trip exposed between them: ~40% of the epilogue)
       uint32_t nmine = 0u;
   #pragma unroll
       for (int i = 0; i < TM; ++i) nmine += __builtin_popcount((und[i] | (und[i] >> 16)) & 0xffffu);
@@ -521,10 +513,29 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           total += (uint32_t)__builtin_popcountll(m) << b;
         }
       }
+      // a tile never straddles buckets (BM, BN <= 256, aligned)
+      const int bucket = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
+      unsigned long long wbase = 0ull;
+      if (total && lane == 0) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
+      CMVE_STAMP(6);
+#ifdef CMVE_DBG_NOFLUSH  // diagnostic build only: no global flush of candidates / counts (results garbage)
+      for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
+      return;
+#endif
+      CMVE_BAR_LDS();  // every wave's row / column count adds have landed in LDS
+      for (int t = tid; t < BM + BN; t += NT) {
+        const int c = lds_rc[t];
+        lds_rc[t] = 0;  // owner thread: ready for the next tile
+        if (!c) continue;
+        if (t < BM) {
+          if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
+        } else {
+          if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
+        }
+      }
       if (total) {
-        uint32_t base = 0u;
-        if (lane == 0) base = atomicAdd(lds_ncand, total);
-        base = __builtin_amdgcn_readfirstlane(base) + excl;
+        unsigned long long slot = __shfl(wbase, 0, 64) + excl;
+        unsigned long long* dst = a.cand + (size_t)bucket * a.cap_b;
   #pragma unroll
         for (int i = 0; i < TM; ++i) {
           uint32_t m = (und[i] | (und[i] >> 16)) & 0xffffu;
@@ -547,43 +558,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
               packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
                        ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
             }
-            if (base < (uint32_t)CAND_LDS) {
-              lds_cand[base] = packed;
-            } else {  // block buffer full: straight to the tile's bucket
-              const int bk = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
-              const unsigned long long slot = atomicAdd(a.bucket_cnt + bk, 1ull);
-              if ((long long)slot < a.cap_b) a.cand[(size_t)bk * a.cap_b + slot] = packed;
-            }
-            ++base;
+            if ((long long)slot < a.cap_b) dst[slot] = packed;
+            ++slot;
           }
-        }
-      }
-      CMVE_STAMP(6);
-#ifdef CMVE_DBG_NOFLUSH  // diagnostic build only: no global flush of candidates / counts (results garbage)
-      if (tid == 0) *lds_ncand = 0u;
-      for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
-      return;
-#endif
-      CMVE_BAR_LDS();
-      // flush the block's undecided pairs with ONE global atomic
-      const unsigned nlds = min(*lds_ncand, (unsigned)CAND_LDS);
-      // a tile never straddles buckets (BM, BN <= 256, aligned)
-      const int bucket = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
-      if (tid == 0 && nlds) *lds_cand_base = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)nlds);
-      CMVE_BAR_LDS();
-      for (unsigned t = tid; t < nlds; t += NT) {
-        const unsigned long long slot = *lds_cand_base + t;
-        if ((long long)slot < a.cap_b) a.cand[(size_t)bucket * a.cap_b + slot] = lds_cand[t];
-      }
-      if (tid == 0) *lds_ncand = 0u;  // every thread read it before the barrier above
-      for (int t = tid; t < BM + BN; t += NT) {
-        const int c = lds_rc[t];
-        lds_rc[t] = 0;  // owner thread: ready for the next tile
-        if (!c) continue;
-        if (t < BM) {
-          if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
-        } else {
-          if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
         }
       }
   #ifdef CMVE_DBG_STAMPS
