@@ -132,25 +132,23 @@ def inference_leg(n_gallery=1048576, d=1024, k=10, reps=20, cpu_rows=262144):
     16-caption batches.  The gallery is packed once (resident); a call = query pack + GEMV + top-k
     select + fp64 re-score + D2H of the ids.  CPU leg: the oracle port of the reference's per-query
     path (re-normalise the gallery, fp64 GEMV, full argsort) on a bounded sample of the gallery."""
-    from cmve import engine
+    from cmve.linas.inference import GalleryScorer
     from oracle import retrieval as R
     dev = torch.device("cuda", torch.cuda.current_device())
     gen = torch.Generator(device=dev).manual_seed(77)
     gal = torch.randn((n_gallery, d), generator=gen, device=dev, dtype=torch.float32)
-    g = engine.RowSet(gal, eps=0.0, with_lo=True, device=dev)
+    scorer = GalleryScorer(gal)  # the inference.py mirror: gallery normalised + packed once
+    g = scorer.gallery
     picks = torch.randint(0, n_gallery, (32,), generator=gen, device=dev)
     caps = (gal[picks] + 10.0 * torch.randn((32, d), generator=gen, device=dev)).contiguous()
     out = {"gallery": n_gallery, "dim": d, "k": k}
-    ws = torch.empty(engine.topk_workspace_floats(engine.RowSet(caps[:16], eps=0.0, with_lo=True, device=dev), g, k),
-                     dtype=torch.float32, device=dev)
     ids1 = None
     for nq in (1, 16):
         times = []
         for r in range(reps + 3):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            q = engine.RowSet(caps[r % 16:r % 16 + nq] if nq == 1 else caps[:nq], eps=0.0, with_lo=True, device=dev)
-            idx, _ = engine.topk(q, g, k, scores_ws=ws)
+            idx = scorer.topk_indices(caps[r % 16:r % 16 + nq] if nq == 1 else caps[:nq], k)
             if r >= 3:
                 times.append(time.perf_counter() - t0)
             if nq == 1 and r == 3:
@@ -169,7 +167,7 @@ def inference_leg(n_gallery=1048576, d=1024, k=10, reps=20, cpu_rows=262144):
                            "sample": f"1 caption x {cpu_rows} videos x {d}-d: fp64 l2norm of the gallery, GEMV, "
                                      f"full argsort (oracle/retrieval.py inference_topk), {dt:.2f} s"}
     out["gpu_over_cpu_nq1"] = out["nq1"]["pairs_per_s"] / out["cpu_baseline"]["value"]
-    del g, gal
+    del g, gal, scorer
     torch.cuda.empty_cache()
     return out
 

@@ -117,6 +117,16 @@ class RowSet:
                          err_h16=self.err_h16.data_ptr() if with_f16 else None)
         check(lib.cmve_pack_rows(handle(device), C.byref(self.desc)), "cmve_pack_rows")
 
+    def repack(self, x):
+        """Copy new rows of the SAME shape into the resident raw buffer and re-pack them in place
+        (query batches re-scored against a resident gallery: no allocation per call)."""
+        src = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(x))
+        if tuple(src.shape) != tuple(self.raw.shape):
+            raise ValueError(f"RowSet.repack: expected {tuple(self.raw.shape)}, got {tuple(src.shape)}")
+        self.raw.copy_(src, non_blocking=True)
+        check(lib.cmve_pack_rows(handle(self.device), C.byref(self.desc)), "cmve_pack_rows")
+        return self
+
     @property
     def has_lo(self):
         return self.lo is not None
@@ -485,7 +495,7 @@ def topk_batch(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, ws: Optio
 
 
 def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Optional[torch.Tensor] = None,
-         to_host: bool = True, batch: Optional[bool] = None):
+         to_host: bool = True, batch: Optional[bool] = None, out=None):
     """Exact top-k gallery indices per query (score desc, index asc) + their fp64 cosines.
     to_host=False returns the device tensors (int32 idx, fp64 scores) instead of numpy arrays.
     Large query batches go through cmve_topk_batch (no score matrix; batch=False forces the
@@ -513,9 +523,12 @@ def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Opti
     need = topk_workspace_floats(q, g, k)
     if scores_ws is None or scores_ws.numel() < need:
         scores_ws = torch.empty(need, dtype=torch.float32, device=q.device)
-    idx = torch.empty((max(q.n, 1), k), dtype=torch.int32, device=q.device)
-    sc = torch.empty((max(q.n, 1), k), dtype=torch.float64, device=q.device)
-    ovf = torch.zeros(1, dtype=torch.int32, device=q.device)
+    if out is not None:  # caller-held (idx int32, scores fp64 [max(n, 1), k], overflow int32 [1]) buffers
+        idx, sc, ovf = out
+    else:
+        idx = torch.empty((max(q.n, 1), k), dtype=torch.int32, device=q.device)
+        sc = torch.empty((max(q.n, 1), k), dtype=torch.float64, device=q.device)
+        ovf = torch.zeros(1, dtype=torch.int32, device=q.device)
     if mode == _lib.SIM_F16 and not (q.has_f16 and g.has_f16):
         mode = _lib.SIM_BF16
     for m in ((mode, _lib.SIM_BF16X3) if (mode != _lib.SIM_BF16X3 and q.has_lo and g.has_lo) else (mode,)):

@@ -37,19 +37,38 @@ class GalleryScorer:
     """A video gallery resident in HBM, normalised once (LINAS l2norm, no eps)."""
 
     def __init__(self, video_embs, video_ids=None, with_lo=True):
-        self.gallery = engine.RowSet(np.asarray(video_embs), eps=0.0, with_lo=with_lo)
+        emb = video_embs if hasattr(video_embs, "data_ptr") else np.asarray(video_embs)
+        self.gallery = engine.RowSet(emb, eps=0.0, with_lo=with_lo)
         self.video_ids = list(video_ids) if video_ids is not None else None
         self._ws = None
+        self._q = {}    # resident query sets by (rows, dim, dtype): re-packed in place per call
+        self._out = {}  # resident top-k outputs by (rows, k)
 
     def topk_indices(self, cap_embs, topK=10):
         """[N_q, topK] gallery indices, best first (== np.argsort(cal_error(...)[i])[:topK])."""
-        cap_embs = np.atleast_2d(np.asarray(cap_embs))
-        q = engine.RowSet(cap_embs, eps=0.0, with_lo=self.gallery.has_lo, device=self.gallery.device)
-        need = engine.topk_workspace_floats(q, self.gallery, min(topK, self.gallery.n))
+        import torch
+        if not torch.is_tensor(cap_embs):
+            cap_embs = np.atleast_2d(np.asarray(cap_embs))
+        elif cap_embs.dim() == 1:
+            cap_embs = cap_embs[None, :]
+        key = (tuple(cap_embs.shape), str(cap_embs.dtype))
+        q = self._q.get(key)
+        if q is None:
+            q = self._q[key] = engine.RowSet(cap_embs, eps=0.0, with_lo=self.gallery.has_lo,
+                                             device=self.gallery.device)
+        else:
+            q.repack(cap_embs)
+        k = min(topK, self.gallery.n)
+        need = engine.topk_workspace_floats(q, self.gallery, k)
         if self._ws is None or self._ws.numel() < need:
-            import torch
             self._ws = torch.empty(need, dtype=torch.float32, device=self.gallery.device)
-        idx, _ = engine.topk(q, self.gallery, topK, mode=SIM_F16, scores_ws=self._ws)
+        out = self._out.get((q.n, k))
+        if out is None:
+            dev = self.gallery.device
+            out = self._out[(q.n, k)] = (torch.empty((max(q.n, 1), k), dtype=torch.int32, device=dev),
+                                         torch.empty((max(q.n, 1), k), dtype=torch.float64, device=dev),
+                                         torch.zeros(1, dtype=torch.int32, device=dev))
+        idx, _ = engine.topk(q, self.gallery, topK, mode=SIM_F16, scores_ws=self._ws, out=out)
         return idx
 
     def topk_ids(self, cap_emb, topK=10):

@@ -224,3 +224,20 @@ def test_topk_batch_edge_shapes(torch_cuda, nq, ng, d, k, qdt, gdt):
     rows = np.arange(nq) if nq * ng <= 40_000_000 else np.linspace(0, nq - 1, 64).astype(int)
     s = R.exact_scores64(qs[rows], gal)
     _check(idx[rows], sc[rows], s, k)
+
+
+def test_gallery_scorer_resident_buffers(torch_cuda):
+    """GalleryScorer re-packs each new caption into its resident query buffers (per shape) and
+    reuses its outputs: consecutive calls, 1- and 3-caption batches, all equal the oracle."""
+    import torch
+    from cmve.linas.inference import GalleryScorer
+    rng = np.random.default_rng(12)
+    gal = rng.standard_normal((6000, 192))
+    sc = GalleryScorer(gal)
+    for t in range(4):
+        nq = 1 if t % 2 == 0 else 3
+        caps = gal[rng.integers(0, 6000, nq)] + 0.9 * rng.standard_normal((nq, 192))
+        arg = caps if t < 2 else torch.from_numpy(caps).cuda()
+        idx = sc.topk_indices(arg, 7)
+        expect = np.argsort(R.cal_error(gal, caps), axis=1, kind="stable")[:, :7]
+        assert np.array_equal(idx, expect), f"call {t}"
