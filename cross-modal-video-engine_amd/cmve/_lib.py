@@ -83,6 +83,9 @@ SIGNATURES = {
     "cmve_topk": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
     "cmve_topk_batch_workspace": (C.c_int, [_P(Rows), _P(Rows), _i32, _P(_i64), _P(_i64)]),
     "cmve_topk_batch": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "cmve_transpose_blocks": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
+    "cmve_pack_tblocks": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _P(Rows)]),
+    "cmve_layernorm_pack": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _P(Rows)]),
     "cmve_pairwise": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i32, _f64, _f64, _vp,
                                 _i32, _i64]),
     "cmve_bn_train_fwd": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _i64, _vp, _vp]),
@@ -110,7 +113,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

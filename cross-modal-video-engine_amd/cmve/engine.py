@@ -145,6 +145,59 @@ class RowSet:
         return out
 
 
+class PackedOperand:
+    """Split-bf16 planes of a raw GEMM operand [n, d] written by a fused kernel (cmve_pack_tblocks,
+    cmve_layernorm_pack) instead of cmve_pack_rows: usable wherever cmve_linear takes a RowSet
+    packed with raw_rows=True (no fp32 rows behind it, no score bound)."""
+
+    def __init__(self, n: int, d: int, device: Optional[torch.device] = None, row_multiple: int = 1):
+        device = device or default_device()
+        n_pad, d_pad = pack_size(n, d)
+        n_pad = -(-n_pad // row_multiple) * row_multiple
+        self.device, self.n, self.d, self.n_pad, self.d_pad = device, n, d, n_pad, d_pad
+        self.hi = torch.empty((n_pad, d_pad), dtype=torch.int16, device=device)
+        self.lo = torch.empty((n_pad, d_pad), dtype=torch.int16, device=device)
+        self.err_max = torch.empty(3, dtype=torch.float32, device=device)
+        self.desc = Rows(n=n, d=d, n_pad=n_pad, d_pad=d_pad, hi=self.hi.data_ptr(), lo=self.lo.data_ptr(), raw=None,
+                         raw_dtype=_lib.CMVE_F32, flags=_lib.PACK_RAW, raw_ld=d, err_max=self.err_max.data_ptr())
+
+    has_lo = True
+    has_f16 = False
+
+    @classmethod
+    def from_blocks_transposed(cls, x: torch.Tensor, block_rows: int, block_cols: int):
+        """Operand rows (b, c) = column c of block b of x viewed as [nb][block_rows][block_cols]
+        (fp32): each row has block_rows elements (cmve_pack_tblocks)."""
+        x = x.detach().float().contiguous()
+        nb = x.numel() // (block_rows * block_cols)
+        op = cls(nb * block_cols, block_rows, x.device, row_multiple=block_cols)
+        check(lib.cmve_pack_tblocks(handle(x.device), _ptr(x), nb, block_rows, block_cols, C.byref(op.desc)),
+              "cmve_pack_tblocks")
+        return op
+
+    @classmethod
+    def layernorm(cls, x: torch.Tensor, weight, bias, eps: float):
+        """LayerNorm(x) rows (fp64 statistics, cmve_layernorm's arithmetic) as a packed operand."""
+        x = x.detach().float().contiguous()
+        n, d = x.shape
+        op = cls(n, d, x.device)
+        w = weight.detach().float().contiguous() if weight is not None else None
+        b = bias.detach().float().contiguous() if bias is not None else None
+        check(lib.cmve_layernorm_pack(handle(x.device), _ptr(x), x.stride(0), n, d, _ptr(w), _ptr(b), float(eps),
+                                      C.byref(op.desc)), "cmve_layernorm_pack")
+        return op
+
+
+def transpose_blocks(x: torch.Tensor, block_rows: int, block_cols: int) -> torch.Tensor:
+    """y[(b, c), :] = column c of block b of x viewed as [nb][block_rows][block_cols] (fp32)."""
+    x = x.detach().float().contiguous()
+    nb = x.numel() // (block_rows * block_cols)
+    y = torch.empty((nb * block_cols, block_rows), dtype=torch.float32, device=x.device)
+    check(lib.cmve_transpose_blocks(handle(x.device), _ptr(x), nb, block_rows, block_cols, _ptr(y)),
+          "cmve_transpose_blocks")
+    return y
+
+
 def _mode_for(q: RowSet, g: RowSet, mode: Optional[int]) -> int:
     if mode is None:
         mode = _lib.SIM_BF16X3 if (q.has_lo and g.has_lo) else _lib.SIM_BF16

@@ -26,13 +26,16 @@ ACT_NONE, ACT_RELU, ACT_QUICKGELU, ACT_SIGMOID = 0, 1, 2, 3
 
 
 def _linear(x, w, b, act=ACT_NONE, resid=None, packed=None):
-    x = x.detach().float().contiguous()
-    xr = engine.RowSet(x, with_lo=True, with_f16=False, raw_rows=True, device=x.device)
+    if isinstance(x, engine.PackedOperand):  # operand already packed by a fused kernel
+        xr = x
+    else:
+        x = x.detach().float().contiguous()
+        xr = engine.RowSet(x, with_lo=True, with_f16=False, raw_rows=True, device=x.device)
     wr = packed.get(w) if packed is not None else _PackedWeight().get(w)
-    out = torch.empty((x.shape[0], w.shape[0]), dtype=torch.float32, device=x.device)
+    out = torch.empty((xr.n, w.shape[0]), dtype=torch.float32, device=xr.device)
     bb = b.detach().float().contiguous() if b is not None else None
     r = resid.contiguous() if resid is not None else None
-    check(lib.cmve_linear(engine.handle(x.device), engine.C.byref(xr.desc), engine.C.byref(wr.desc), SIM_BF16X3,
+    check(lib.cmve_linear(engine.handle(xr.device), engine.C.byref(xr.desc), engine.C.byref(wr.desc), SIM_BF16X3,
                           engine._ptr(bb), None, None, engine._ptr(r), r.stride(0) if r is not None else 0, act,
                           engine._ptr(out), out.stride(0)), "cmve_linear")
     return out
@@ -142,12 +145,13 @@ class Combiner(nn.Module):
             raise ValueError("combine_batches: rows must be a multiple of the batch size")
         G = b // gs
         n = b * f
-        # conv1x1 over the raw reshape (b*f, -1, 4, 4) (combiner.py:159): channel c = elements c*16 .. c*16+15
+        # conv1x1 over the raw reshape (b*f, -1, 4, 4) (combiner.py:159): channel c = elements c*16 .. c*16+15,
+        # so the GEMM rows are the 16 columns of each [C, 16] block -- packed straight from ref_mid
         C = ref_mid[0, 0].numel() // 16
-        xt = ref_mid.reshape(n, C, 16).transpose(1, 2).reshape(n * 16, C)
+        xt = engine.PackedOperand.from_blocks_transposed(ref_mid, C, 16)
         wc = self.m_remained.weight.view(self.m_remained.weight.shape[0], -1)
         y = _linear(xt, wc, self.m_remained.bias, ACT_RELU, packed=self._p("m_remained"))
-        p_s_m = y.view(n, 16, -1).transpose(1, 2).reshape(b, f, l, -1)              # relu(conv).reshape(b,f,l,-1)
+        p_s_m = engine.transpose_blocks(y, 16, y.shape[1]).view(b, f, l, -1)    # relu(conv).reshape(b,f,l,-1)
         p_r_m = _linear(text, self.m_residual.weight, self.m_residual.bias, ACT_RELU, packed=self._p("m_residual"))
         # ResidualAttentionBlock(q = p_r_m [1,b,d], k = v = p_s_m.reshape(l*f, b, d))  combiner.py:38-43,164-165
         blk = self.self_attn_1
@@ -155,7 +159,7 @@ class Combiner(nn.Module):
         # reshape is taken separately and interleaved: row t*b + g*gs + bb
         kv_in = p_s_m.reshape(l * f * b, d) if G == 1 else \
             p_s_m.reshape(G, l * f, gs, d).transpose(0, 1).reshape(l * f * b, d)
-        kv_ln = _layernorm(kv_in, blk.ln_1)
+        kv_ln = engine.PackedOperand.layernorm(kv_in, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps)
         q_ln = _layernorm(p_r_m, blk.ln_1)
         W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
         q = _linear(q_ln, W[:d], Bi[:d], packed=self._p("in_q"))

@@ -7,6 +7,12 @@
 //                       key t of batch b at row t*B + b of the projected K/V matrix -- exactly the
 //                       raw p_s_m.reshape(l*f, b, d) of combiner.py:164-165 (mixes batch rows)
 //   cmve_fuse_combine   out = normalize( y + ds*text + (1-ds)*ref + relu(based) )   (combiner.py:166,178-180)
+//   cmve_transpose_blocks / cmve_pack_tblocks / cmve_layernorm_pack: the raw reshapes around the
+//                       conv1x1 (combiner.py:159: mid.reshape(b*f, -1, 4, 4) -> its GEMM rows are the
+//                       COLUMNS of each [640, 16] block; the output goes back through .reshape) as
+//                       LDS-tiled block transposes, the transpose of the conv input fused with the
+//                       split-bf16 packing of the GEMM operand, and the key LayerNorm fused with the
+//                       packing of the K/V in-projection's operand (no fp32 round trip)
 #include "cmve_internal.h"
 
 namespace cmve {
@@ -134,6 +140,90 @@ __global__ __launch_bounds__(256) void fuse_combine_kernel(const float* __restri
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// block transposes: block b of x is [R][C] row-major; out row (b, c) = column c of block b.
+// One workgroup per block, staged through LDS with a padded row (C + 1) so the column reads
+// are conflict-free; OUT_PACK writes the split-bf16 planes of a raw GEMM operand
+// (hi = bf16(v), lo = bf16(v - hi): pack_rows_kernel's CMVE_PACK_RAW split), else fp32.
+// ---------------------------------------------------------------------------
+constexpr int TB_MAX = 12288;  // R * C floats staged per block (48 KiB + padding)
+
+template <bool OUT_PACK>
+__global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ x, int64_t nb, int R, int C,
+                                                      float* __restrict__ y, uint16_t* __restrict__ hi,
+                                                      uint16_t* __restrict__ lo, int64_t d_pad) {
+  extern __shared__ float tb[];  // [R][C + 1]
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int W = R * C;
+  if (b < nb) {
+    const float* xb = x + b * (int64_t)W;
+    for (int e = tid; e < W; e += 256) tb[(e / C) * (C + 1) + (e % C)] = xb[e];
+    __syncthreads();
+  }
+  const int ow = OUT_PACK ? (int)d_pad : R;  // output row width
+  for (int e = tid; e < C * ow; e += 256) {
+    const int c = e / ow, k = e - c * ow;
+    const float v = (b < nb && k < R) ? tb[k * (C + 1) + c] : 0.f;
+    const int64_t o = (b * C + c) * (int64_t)ow + k;
+    if constexpr (OUT_PACK) {
+      const uint16_t h = f2bf(v);
+      hi[o] = h;
+      lo[o] = f2bf(v - bf2f(h));
+    } else {
+      y[o] = v;
+    }
+  }
+}
+
+// LayerNorm of rows of x (the register-row path of layernorm_kernel, same arithmetic) written as
+// the split-bf16 planes of a raw GEMM operand; rows [n, n_pad) and columns [d, d_pad) are zero.
+__global__ __launch_bounds__(256) void layernorm_pack_kernel(const float* __restrict__ x, int64_t ldx, int64_t n,
+                                                             int64_t d, int64_t n_pad, int64_t d_pad,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, double eps,
+                                                             uint16_t* __restrict__ hi, uint16_t* __restrict__ lo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_pad) return;
+  uint16_t* hr = hi + row * d_pad;
+  uint16_t* lr = lo + row * d_pad;
+  if (row >= n) {
+    for (int64_t k = lane; k < d_pad; k += 64) hr[k] = lr[k] = 0;
+    return;
+  }
+  const float* xr = x + row * ldx;
+  float v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = (lane + 64 * m < d) ? xr[lane + 64 * m] : 0.f;
+  double s = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m)
+    if (lane + 64 * m < d) s += (double)v[m];
+  const double mean = wave_sum(s) / (double)d;
+  double q = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m)
+    if (lane + 64 * m < d) {
+      const double c = (double)v[m] - mean;
+      q = fma(c, c, q);
+    }
+  const double rstd = 1.0 / sqrt(wave_sum(q) / (double)d + eps);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int64_t k = lane + 64 * m;
+    if (k < d) {
+      const double c = ((double)v[m] - mean) * rstd;
+      const float y = (float)(c * (double)(gamma ? gamma[k] : 1.f) + (double)(beta ? beta[k] : 0.f));
+      const uint16_t h = f2bf(y);
+      hr[k] = h;
+      lr[k] = f2bf(y - bf2f(h));
+    }
+  }
+  for (int64_t k = d + lane; k < d_pad; k += 64) hr[k] = lr[k] = 0;
+}
+
 }  // namespace cmve
 
 using namespace cmve;
@@ -167,4 +257,54 @@ extern "C" int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* d
   hipLaunchKernelGGL(fuse_combine_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream, y, ds, text, ref,
                      based, n, d, eps, out);
   return check_launch("fuse_combine");
+}
+
+
+// a raw (CMVE_PACK_RAW) GEMM operand written by a fused kernel: no score bound (err_max = +inf)
+static int raw_operand_ready(cmve_handle_t h, cmve_rows_t* r) {
+  r->flags |= CMVE_PACK_RAW;
+  if (r->err_max) CMVE_HIP(hipMemsetD32Async((hipDeviceptr_t)r->err_max, 0x7f800000u, 3, h->stream));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_transpose_blocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, float* y) {
+  CMVE_REQUIRE(h && x && y, "cmve_transpose_blocks: NULL argument");
+  CMVE_REQUIRE(nb >= 0 && R > 0 && C > 0 && R * C <= TB_MAX && R * (C + 1) * 4 <= 65536,
+               "cmve_transpose_blocks: bad block shape");
+  if (nb == 0) return CMVE_OK;
+  const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
+  hipLaunchKernelGGL(tblocks_kernel<false>, dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R, (int)C, y,
+                     nullptr, nullptr, (int64_t)0);
+  return check_launch("transpose_blocks");
+}
+
+extern "C" int cmve_pack_tblocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, cmve_rows_t* out) {
+  CMVE_REQUIRE(h && x && out && out->hi && out->lo, "cmve_pack_tblocks: NULL argument");
+  CMVE_REQUIRE(nb >= 0 && R > 0 && C > 0 && R * C <= TB_MAX && R * (C + 1) * 4 <= 65536,
+               "cmve_pack_tblocks: bad block shape");
+  CMVE_REQUIRE(out->n == nb * C && out->d == R && out->d_pad >= R && out->n_pad >= out->n && out->n_pad % C == 0,
+               "cmve_pack_tblocks: out must describe nb*C rows of R (n_pad a multiple of C)");
+  const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
+  const int64_t grid = out->n_pad / C;  // blocks past nb write the zero padding rows
+  if (grid) {
+    hipLaunchKernelGGL(tblocks_kernel<true>, dim3((unsigned)grid), dim3(256), lds, h->stream, x, nb, (int)R, (int)C,
+                       nullptr, out->hi, out->lo, out->d_pad);
+    int st = check_launch("pack_tblocks");
+    if (st) return st;
+  }
+  return raw_operand_ready(h, out);
+}
+
+extern "C" int cmve_layernorm_pack(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d,
+                                   const float* gamma, const float* beta, double eps, cmve_rows_t* out) {
+  CMVE_REQUIRE(h && x && out && out->hi && out->lo, "cmve_layernorm_pack: NULL argument");
+  CMVE_REQUIRE(n >= 0 && d > 0 && d <= 1024 && ldx >= d, "cmve_layernorm_pack: bad shape (d <= 1024)");
+  CMVE_REQUIRE(out->n == n && out->d == d && out->d_pad >= d && out->n_pad >= n, "cmve_layernorm_pack: bad out");
+  if (out->n_pad) {
+    hipLaunchKernelGGL(layernorm_pack_kernel, dim3((unsigned)((out->n_pad + 3) / 4)), dim3(256), 0, h->stream, x,
+                       ldx, n, d, out->n_pad, out->d_pad, gamma, beta, eps, out->hi, out->lo);
+    int st = check_launch("layernorm_pack");
+    if (st) return st;
+  }
+  return raw_operand_ready(h, out);
 }

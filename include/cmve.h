@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 5
+#define CMVE_ABI_VERSION 6
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -176,6 +176,23 @@ int cmve_mha_1q(cmve_handle_t h, const float* q, int64_t ldq, const float* kv, i
                 int32_t B, int32_t T, int32_t H, int32_t dh, float* out, int64_t ldo);
 int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* ds, const float* text, const float* ref,
                       const float* based, int64_t n, int64_t d, double eps, float* out);
+/*
+ * The raw reshapes around Combiner's conv1x1 (MultiFusion/src/combiner.py:159,164): block b of x is
+ * [R][C] row-major and its column c becomes row (b, c) of the output.
+ *   cmve_transpose_blocks: fp32 out y [nb * C, R] (relu(conv(...)).reshape(b, f, l, -1) of the conv's
+ *     [nb * 16, 640] output: R = 16, C = 640);
+ *   cmve_pack_tblocks: out = the split-bf16 planes of the raw GEMM operand [nb * C, R] (the conv's
+ *     input mid.reshape(b*f, 640, 16): R = 640, C = 16), written straight from x with no fp32
+ *     transpose in between; out->{n, d, n_pad, d_pad} from cmve_pack_size, n_pad % C == 0;
+ *   cmve_layernorm_pack: cmve_layernorm written as such planes (the K/V in-projection's operand).
+ * The packed outputs carry CMVE_PACK_RAW (GEMM operands of cmve_linear only, err_max = +inf) and
+ * hold bit for bit what cmve_pack_rows(CMVE_PACK_RAW) would make of the fp32 result.
+ * R * (C + 1) * 4 <= 64 KiB; cmve_layernorm_pack: d <= 1024.
+ */
+int cmve_transpose_blocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, float* y);
+int cmve_pack_tblocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, cmve_rows_t* out);
+int cmve_layernorm_pack(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, const float* gamma,
+                        const float* beta, double eps, cmve_rows_t* out);
 
 /*
  * K6 -- TripletLoss (LINAS-engine/loss.py:83-153) over a square score matrix S [B, B]

@@ -67,3 +67,32 @@ def test_gpu_combine_batches_equals_batch_loop(state):
                       for i in range(0, high.shape[0], 32)])
     fused = m.combine_batches((high, mid), text, batch_size=32)
     assert torch.equal(loop, fused)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_transpose_and_layernorm_packing():
+    """cmve_pack_tblocks / cmve_layernorm_pack write the same split-bf16 planes cmve_pack_rows
+    (raw rows) makes of the fp32 transpose / LayerNorm, bit for bit, padding rows / columns zero;
+    cmve_transpose_blocks equals the torch transpose."""
+    import torch
+    from cmve import engine
+    from cmve.multifusion.combiner import _layernorm
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.standard_normal((37, 16, 640)).astype(np.float32)).cuda()
+    ref_t = x.reshape(37, 640, 16).transpose(1, 2).reshape(37 * 16, 640).contiguous()
+    op = engine.PackedOperand.from_blocks_transposed(x, 640, 16)
+    rs = engine.RowSet(ref_t, with_lo=True, with_f16=False, raw_rows=True)
+    assert op.n == rs.n and op.n_pad >= rs.n_pad
+    assert torch.equal(op.hi[:rs.n_pad], rs.hi) and torch.equal(op.lo[:rs.n_pad], rs.lo)
+    assert not op.hi[rs.n_pad:].any()
+    y = torch.from_numpy(rng.standard_normal((37 * 16, 640)).astype(np.float32)).cuda()
+    assert torch.equal(engine.transpose_blocks(y, 16, 640),
+                       y.view(37, 16, 640).transpose(1, 2).reshape(37 * 640, 16))
+    ln = torch.nn.LayerNorm(200).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    z = torch.from_numpy(rng.standard_normal((333, 200)).astype(np.float32)).cuda()
+    pk = engine.PackedOperand.layernorm(z, ln.weight, ln.bias, ln.eps)
+    rz = engine.RowSet(_layernorm(z, ln), with_lo=True, with_f16=False, raw_rows=True)
+    assert torch.equal(pk.hi, rz.hi) and torch.equal(pk.lo, rz.lo)
