@@ -115,6 +115,85 @@ __global__ __launch_bounds__(256) void mha_1q_kernel(const float* __restrict__ q
     out[(int64_t)b * ldo + h * dh + e] = (po[e] + po[dh + e]) + (po[2 * dh + e] + po[3 * dh + e]);
 }
 
+// Same attention, block per batch element b with ALL heads: lane l owns elements [E l, E l + E)
+// of every K / V row (E = d / 64, a head = dh / E consecutive lanes), so each key row is one
+// coalesced 4*d-byte read per wave and a head's q.k is a DPP sum over its lanes; the softmax and
+// the V accumulation keep mha_1q_kernel's arithmetic and order (only the q.k partial-sum order
+// differs).  The per-(b, h) kernel read 80-float row pieces and reduced each key over 64 lanes
+// with LDS permutes: ~2.2 TB/s on the C4 shape.
+__device__ __forceinline__ float group_sum_f32(float v, int lph) {
+  auto dpp = [](float x, int ctrl) -> float {
+    switch (ctrl) {
+      case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+      case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+      case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
+    }
+  };
+  if (lph >= 2) v += dpp(v, 0);   // quad_perm [1,0,3,2]
+  if (lph >= 4) v += dpp(v, 1);   // quad_perm [2,3,0,1]
+  if (lph >= 8) v += dpp(v, 2);   // row_half_mirror
+  if (lph >= 16) v += dpp(v, 3);  // row_mirror
+  return v;
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void mha_1q_rows_kernel(const float* __restrict__ q, int64_t ldq,
+                                                          const float* __restrict__ kv, int64_t ldkv, int64_t v_off,
+                                                          int B, int T, int H, int dh, float* __restrict__ out,
+                                                          int64_t ldo) {
+  extern __shared__ float sh[];  // scores [H][T] + partial out [4][d]
+  constexpr int D = 64 * E;
+  float* sc = sh;
+  float* po = sc + (size_t)H * T;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lph = dh / E, head = lane / lph;
+  const float scaling = 1.0f / sqrtf((float)dh);
+  float qv[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) qv[i] = q[(int64_t)b * ldq + lane * E + i] * scaling;
+  for (int t = wave; t < T; t += 4) {
+    const float* kr = kv + ((int64_t)t * B + b) * ldkv + lane * E;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc = fmaf(qv[i], kr[i], acc);
+    acc = group_sum_f32(acc, lph);
+    if (lane % lph == 0) sc[head * T + t] = acc;
+  }
+  __syncthreads();
+  for (int hh = wave; hh < H; hh += 4) {  // softmax over T: mha_1q_kernel's arithmetic, one wave per head
+    float* s_h = sc + (size_t)hh * T;
+    float m = -INFINITY;
+    for (int t = lane; t < T; t += 64) m = fmaxf(m, s_h[t]);
+    m = wave_max(m);
+    double s = 0.0;
+    for (int t = lane; t < T; t += 64) {
+      const float p = expf(s_h[t] - m);
+      s_h[t] = p;
+      s += (double)p;
+    }
+    s = wave_sum(s);
+    const float inv = (float)(1.0 / s);
+    for (int t = lane; t < T; t += 64) s_h[t] *= inv;
+  }
+  __syncthreads();
+  float acc[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) acc[i] = 0.f;
+  for (int t = wave; t < T; t += 4) {
+    const float p = sc[head * T + t];
+    const float* vr = kv + ((int64_t)t * B + b) * ldkv + v_off + lane * E;
+#pragma unroll
+    for (int i = 0; i < E; ++i) acc[i] = fmaf(p, vr[i], acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < E; ++i) po[wave * D + lane * E + i] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < D; e += 256)
+    out[(int64_t)b * ldo + e] = (po[e] + po[D + e]) + (po[2 * D + e] + po[3 * D + e]);
+}
+
 // out = normalize( ((y + ds*text) + (1-ds)*ref) + based , eps )
 __global__ __launch_bounds__(256) void fuse_combine_kernel(const float* __restrict__ y, const float* __restrict__ ds,
                                                            const float* __restrict__ text,
@@ -243,6 +322,20 @@ extern "C" int cmve_mha_1q(cmve_handle_t h, const float* q, int64_t ldq, const f
   CMVE_REQUIRE(h && q && kv && out, "cmve_mha_1q: NULL argument");
   CMVE_REQUIRE(B > 0 && T > 0 && H > 0 && dh > 0 && ldq >= (int64_t)H * dh && ldo >= (int64_t)H * dh,
                "cmve_mha_1q: bad shape");
+  const int64_t d = (int64_t)H * dh;
+  const int E = (int)(d / 64);
+  const int lph = (d % 64 == 0 && E > 0 && dh % E == 0) ? dh / E : 0;
+  const size_t lds_rows = sizeof(float) * ((size_t)H * T + 4 * (size_t)d);
+  if ((E == 10 || E == 8 || E == 16 || E == 4) && (lph == 1 || lph == 2 || lph == 4 || lph == 8 || lph == 16) &&
+      lds_rows <= 64 * 1024) {  // all heads per block (Combiner: d 640 = 8 x 80, E 10)
+#define MR(EE)                                                                                                       hipLaunchKernelGGL(mha_1q_rows_kernel<EE>, dim3((unsigned)B), dim3(256), lds_rows, h->stream, q, ldq, kv, ldkv,                      v_off, B, T, H, dh, out, ldo)
+    if (E == 10) MR(10);
+    else if (E == 8) MR(8);
+    else if (E == 16) MR(16);
+    else MR(4);
+#undef MR
+    return check_launch("mha_1q_rows");
+  }
   const size_t lds = sizeof(float) * ((size_t)T + dh + 4 * (size_t)dh);
   CMVE_REQUIRE(lds <= 64 * 1024, "cmve_mha_1q: T/dh too large for one block");
   hipLaunchKernelGGL(mha_1q_kernel, dim3((unsigned)B, (unsigned)H), dim3(256), lds, h->stream, q, ldq, kv, ldkv, v_off,
