@@ -85,6 +85,7 @@ SIGNATURES = {
     "cmve_topk_batch": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
     "cmve_transpose_blocks": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
     "cmve_pack_tblocks": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _P(Rows)]),
+    "cmve_transpose_blocks_kv": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "cmve_layernorm_pack": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _P(Rows)]),
     "cmve_pairwise": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _i64, _i32, _f64, _f64, _vp,
                                 _i32, _i64]),

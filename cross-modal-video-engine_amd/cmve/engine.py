@@ -188,6 +188,18 @@ class PackedOperand:
         return op
 
 
+def transpose_blocks_kv(x: torch.Tensor, block_rows: int, block_cols: int, d: int, T: int, gs: int,
+                        B: int) -> torch.Tensor:
+    """transpose_blocks whose output rows of d floats (g, t, bb) of .reshape(B // gs, T, gs, d) are
+    stored at row t*B + g*gs + bb (cmve_transpose_blocks_kv): [T * B, d]."""
+    x = x.detach().float().contiguous()
+    nb = x.numel() // (block_rows * block_cols)
+    y = torch.empty((T * B, d), dtype=torch.float32, device=x.device)
+    check(lib.cmve_transpose_blocks_kv(handle(x.device), _ptr(x), nb, block_rows, block_cols, d, T, gs, B, _ptr(y)),
+          "cmve_transpose_blocks_kv")
+    return y
+
+
 def transpose_blocks(x: torch.Tensor, block_rows: int, block_cols: int) -> torch.Tensor:
     """y[(b, c), :] = column c of block b of x viewed as [nb][block_rows][block_cols] (fp32)."""
     x = x.detach().float().contiguous()

@@ -151,14 +151,13 @@ class Combiner(nn.Module):
         xt = engine.PackedOperand.from_blocks_transposed(ref_mid, C, 16)
         wc = self.m_remained.weight.view(self.m_remained.weight.shape[0], -1)
         y = _linear(xt, wc, self.m_remained.bias, ACT_RELU, packed=self._p("m_remained"))
-        p_s_m = engine.transpose_blocks(y, 16, y.shape[1]).view(b, f, l, -1)    # relu(conv).reshape(b,f,l,-1)
         p_r_m = _linear(text, self.m_residual.weight, self.m_residual.bias, ACT_RELU, packed=self._p("m_residual"))
-        # ResidualAttentionBlock(q = p_r_m [1,b,d], k = v = p_s_m.reshape(l*f, b, d))  combiner.py:38-43,164-165
+        # ResidualAttentionBlock(q = p_r_m [1,b,d], k = v = p_s_m.reshape(l*f, b, d))  combiner.py:38-43,164-165,
+        # p_s_m = relu(conv).reshape(b, f, l, -1): the key/value rows, row t*b + bb == [t, bb] of the raw
+        # reshape(l*f, b, d); with G batches of gs rows each batch's raw reshape is taken separately and
+        # interleaved, row t*b + g*gs + bb -- written in that order straight from the conv output
         blk = self.self_attn_1
-        # row t*b + bb == [t, bb] of reshape(l*f, b, d); with G batches of gs rows each batch's raw
-        # reshape is taken separately and interleaved: row t*b + g*gs + bb
-        kv_in = p_s_m.reshape(l * f * b, d) if G == 1 else \
-            p_s_m.reshape(G, l * f, gs, d).transpose(0, 1).reshape(l * f * b, d)
+        kv_in = engine.transpose_blocks_kv(y, 16, y.shape[1], d, l * f, gs, b)
         kv_ln = engine.PackedOperand.layernorm(kv_in, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps)
         q_ln = _layernorm(p_r_m, blk.ln_1)
         W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias

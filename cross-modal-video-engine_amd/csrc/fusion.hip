@@ -228,10 +228,15 @@ __global__ __launch_bounds__(256) void fuse_combine_kernel(const float* __restri
 // ---------------------------------------------------------------------------
 constexpr int TB_MAX = 12288;  // R * C floats staged per block (48 KiB + padding)
 
+// kv remap (fp32 out only, kv_d > 0): the transposed blocks form a flat array whose consecutive
+// kv_d-float runs u are the raw p_s_m.reshape(G, T, gs, d) rows (g, t, bb) = (u / (T gs),
+// (u / gs) % T, u % gs); run u is written to row t*kvB + g*gs + bb -- the key/value order of
+// combiner.py:164-165 for G consecutive batches of gs rows (G = 1: the plain reshape).
 template <bool OUT_PACK>
 __global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ x, int64_t nb, int R, int C,
                                                       float* __restrict__ y, uint16_t* __restrict__ hi,
-                                                      uint16_t* __restrict__ lo, int64_t d_pad) {
+                                                      uint16_t* __restrict__ lo, int64_t d_pad, int kv_d = 0,
+                                                      int kv_T = 1, int kv_gs = 1, int kv_B = 1) {
   extern __shared__ float tb[];  // [R][C + 1]
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -245,12 +250,18 @@ __global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ 
   for (int e = tid; e < C * ow; e += 256) {
     const int c = e / ow, k = e - c * ow;
     const float v = (b < nb && k < R) ? tb[k * (C + 1) + c] : 0.f;
-    const int64_t o = (b * C + c) * (int64_t)ow + k;
+    int64_t o = (b * C + c) * (int64_t)ow + k;
     if constexpr (OUT_PACK) {
       const uint16_t h = f2bf(v);
       hi[o] = h;
       lo[o] = f2bf(v - bf2f(h));
     } else {
+      if (kv_d > 0) {  // 32-bit index math (the host checks nb * R * C < 2^32)
+        const uint32_t ou = (uint32_t)o, u = ou / (uint32_t)kv_d, w = ou - u * (uint32_t)kv_d;
+        const uint32_t tg = (uint32_t)kv_T * (uint32_t)kv_gs, g = u / tg, rem = u - g * tg;
+        const uint32_t t = rem / (uint32_t)kv_gs, bb = rem - t * (uint32_t)kv_gs;
+        o = ((int64_t)t * kv_B + (int64_t)g * kv_gs + bb) * kv_d + w;
+      }
       y[o] = v;
     }
   }
@@ -369,6 +380,21 @@ extern "C" int cmve_transpose_blocks(cmve_handle_t h, const float* x, int64_t nb
   hipLaunchKernelGGL(tblocks_kernel<false>, dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R, (int)C, y,
                      nullptr, nullptr, (int64_t)0);
   return check_launch("transpose_blocks");
+}
+
+extern "C" int cmve_transpose_blocks_kv(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, int64_t d,
+                                        int64_t T, int64_t gs, int64_t B, float* y) {
+  CMVE_REQUIRE(h && x && y, "cmve_transpose_blocks_kv: NULL argument");
+  CMVE_REQUIRE(nb >= 0 && R > 0 && C > 0 && R * C <= TB_MAX && R * (C + 1) * 4 <= 65536,
+               "cmve_transpose_blocks_kv: bad block shape");
+  CMVE_REQUIRE(d > 0 && T > 0 && gs > 0 && B % gs == 0 && (nb * R * C) == B * T * d,
+               "cmve_transpose_blocks_kv: nb*R*C must equal B*T*d with gs | B");
+  CMVE_REQUIRE(nb * R * C < (1ll << 32), "cmve_transpose_blocks_kv: more than 2^32 elements (split the batch)");
+  if (nb == 0) return CMVE_OK;
+  const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
+  hipLaunchKernelGGL(tblocks_kernel<false>, dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R, (int)C, y,
+                     nullptr, nullptr, (int64_t)0, (int)d, (int)T, (int)gs, (int)B);
+  return check_launch("transpose_blocks_kv");
 }
 
 extern "C" int cmve_pack_tblocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, cmve_rows_t* out) {

@@ -191,6 +191,12 @@ int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* ds, const fl
  */
 int cmve_transpose_blocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, float* y);
 int cmve_pack_tblocks(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, cmve_rows_t* out);
+/* cmve_transpose_blocks with the attention's key order: the transposed output, read as rows of d
+ * floats u = (g, t, bb) of p_s_m.reshape(G, T, gs, d), lands in row t*B + g*gs + bb (G = B / gs
+ * consecutive batches of gs rows; gs = B is the reference's single-batch reshape(l*f, b, d),
+ * combiner.py:164-165).  nb * R * C == B * T * d. */
+int cmve_transpose_blocks_kv(cmve_handle_t h, const float* x, int64_t nb, int64_t R, int64_t C, int64_t d, int64_t T,
+                             int64_t gs, int64_t B, float* y);
 int cmve_layernorm_pack(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, const float* gamma,
                         const float* beta, double eps, cmve_rows_t* out);
 
