@@ -50,19 +50,31 @@ def _as_int64(names) -> np.ndarray:
         return np.asarray([int(v) for v in names], np.int64)
 
 
+class _NameIndex:
+    """index_names -> row lookups, vectorised: the last row of a repeated name (as a {name: row}
+    dict built in order), -1 when absent."""
+
+    def __init__(self, index_names: Sequence):
+        keys = _as_int64(index_names)
+        self.order = np.argsort(keys, kind="stable")
+        self.sorted = keys[self.order]
+
+    def rows(self, names: Sequence) -> np.ndarray:
+        want = _as_int64(names)
+        if self.sorted.size == 0:
+            return np.full(want.shape, -1, np.int64)
+        at = np.searchsorted(self.sorted, want, side="right") - 1
+        atc = np.clip(at, 0, None)
+        hit = (at >= 0) & (self.sorted[atc] == want)
+        return np.where(hit, self.order[atc], -1)
+
+
 def _positions(index_names: Sequence, names: Sequence) -> np.ndarray:
-    """Row of each name in index_names (-1 when absent; the last row of a repeated name, as a
-    {name: row} dict built in order), vectorised (30k lookups per val pass)."""
-    keys = _as_int64(index_names)
-    want = _as_int64(names)
-    if keys.size == 0:
-        return np.full(want.shape, -1, np.int64)
-    order = np.argsort(keys, kind="stable")
-    sk = keys[order]
-    at = np.searchsorted(sk, want, side="right") - 1
-    atc = np.clip(at, 0, None)
-    hit = (at >= 0) & (sk[atc] == want)
-    return np.where(hit, order[atc], -1)
+    """Row of each name in index_names (see _NameIndex)."""
+    return _NameIndex(index_names).rows(names)
+
+
+_WS = {}  # undecided-pair lists kept per device across validation passes (grown once, then reused)
 
 
 def cirr_target_ranks(predicted_features: torch.Tensor, index_pooled: torch.Tensor, index_names: Sequence,
@@ -71,8 +83,9 @@ def cirr_target_ranks(predicted_features: torch.Tensor, index_pooled: torch.Tens
     One fused rank-count pass (exact fp64 decisions) plus the reference's own score:
         rank = 1 + #{j : s_j > s_target} - [s_ref > s_target]     (validate.py:76-87)"""
     dev = predicted_features.device if torch.is_tensor(predicted_features) else engine.default_device()
-    tgt = _positions(index_names, target_names)
-    ref = _positions(index_names, reference_names)
+    ix = _NameIndex(index_names)
+    tgt = ix.rows(target_names)
+    ref = ix.rows(reference_names)
     q = engine.RowSet(predicted_features, eps=1e-12, with_lo=False, device=dev)
     g = engine.RowSet(index_pooled, eps=1e-12, with_lo=False, device=dev)
     mode = engine._lib.SIM_F16
@@ -85,7 +98,9 @@ def cirr_target_ranks(predicted_features: torch.Tensor, index_pooled: torch.Tens
 
     s_t, hi, lo = engine.gt_thresholds(q, g, *one_gt(tgt), mode)
     s_r, _, _ = engine.gt_thresholds(q, g, *one_gt(ref), mode)
-    ws = engine.RankWorkspace(dev, cap=max(1 << 16, 64 * (q.n + g.n)))
+    ws = _WS.get(str(dev))
+    if ws is None or ws.cap < 64 * (q.n + g.n):
+        ws = _WS[str(dev)] = engine.RankWorkspace(dev, cap=max(1 << 16, 64 * (q.n + g.n)))
     for _attempt in range(4):
         cnt, _ = engine.rank_count_launch(q, g, mode, row=(s_t, hi, lo), ws=ws)
         ncand = ws.ncand()
