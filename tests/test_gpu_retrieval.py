@@ -397,3 +397,32 @@ def test_raw_packed_sets_rejected_by_rank_and_topk(torch_cuda):
         engine.gt_rank_counts(raw, unit, row_gts=[[0]] * 300)
     with pytest.raises(_lib.CmveError, match="PACK_RAW"):
         engine.topk(unit, raw, 5)
+
+
+def test_bench_shape_ranks_against_independent_fp64(torch_cuda):
+    """The bench's own shape (16,384 captions x a 131,072-video shard x 1024-d, G256 persistent
+    rank kernel + bucketed fix-up, sigma 10): the fused t2v ranks of 512 sampled captions equal
+    counts from an independent fp64 GEMM on the GPU."""
+    from cmve import engine, _lib
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(9)
+    nq, ng, d = 16384, 131072, 1024
+    gal = torch.randn((ng, d), generator=gen, device=dev)
+    gt = torch.randint(0, ng, (nq,), generator=gen, device=dev)
+    q = gal[gt] + 10.0 * torch.randn((nq, d), generator=gen, device=dev)
+    caps = engine.RowSet(q, eps=0.0, with_lo=False, device=dev)
+    vids = engine.RowSet(gal, eps=0.0, with_lo=False, device=dev)
+    gts = [[int(x)] for x in gt.cpu().numpy()]
+    t2v, _, ncand = engine.gt_rank_counts(caps, vids, row_gts=gts, mode=_lib.SIM_F16)
+    assert ncand > 100000  # the fix-up path is exercised
+    rows = torch.arange(0, nq, nq // 512, device=dev)
+    qd = q[rows].double()
+    qd = qd / qd.norm(dim=1, keepdim=True)
+    exp = np.empty(rows.numel(), np.int64)
+    for b in range(0, rows.numel(), 128):
+        s = qd[b:b + 128] @ (gal.double() / gal.double().norm(dim=1, keepdim=True)).T
+        sg = s.gather(1, gt[rows[b:b + 128]][:, None])
+        exp[b:b + 128] = 1 + (s > sg).sum(dim=1).cpu().numpy()
+    got = t2v[rows.cpu().numpy()]
+    assert (got != exp).sum() <= 1, np.nonzero(got != exp)
