@@ -189,6 +189,35 @@ def sharded_topk_leg(scorer, q_local, nq, n_global, k=10, reps=5):
             "note": "wall clock incl. Q all-gather, sample + main MFMA passes, fp64 band re-score, merge, D2H"}
 
 
+def other_configs_leg():
+    """BASELINE configs C2 and C4 on this GPU (the full-size runs are tools/train_bench.py and
+    tools/fusion_bench.py): the C2 training step (B 128, 1024 -> 1024 heads, InfoNCE row + col and
+    TripletLoss, clip + Adam, one hipGraph replay per step) and the C4 MultiFusion composed path on
+    8,192 queries x the 44,493-video gallery.  Failures are reported, never fatal to the bench line."""
+    import argparse as _ap
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    out = {}
+    try:
+        import train_bench as TB
+        dev = torch.device("cuda", torch.cuda.current_device())
+        batches = TB.data(dev, 4)
+        c2 = {}
+        for loss_name in ("infonce", "triplet"):
+            ms, _ = TB.time_leg(TB.cmve_step_fn(dev, loss_name, graph=True), batches, 10, 50, dev)
+            c2[loss_name] = {"ms_per_step": ms, "samples_per_s": TB.B / ms * 1e3}
+        out["c2_train_step"] = c2
+    except Exception as e:  # noqa: BLE001
+        out["c2_train_step"] = {"error": repr(e)}
+    try:
+        import fusion_bench as FB
+        c4 = FB.run(_ap.Namespace(nq=8192, nv=44493, chunk=8192, loop_q=256))
+        out["c4_multifusion"] = {k: c4[k] for k in ("nq", "nv", "combine_batches", "ranking", "end_to_end")}
+    except Exception as e:  # noqa: BLE001
+        out["c4_multifusion"] = {"error": repr(e)}
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(gallery_np, queries_np, gts_local, n_sample):
     """Oracle port of the reference CPU path: fp64 cal_error (evaluation.py:17-21) + per-row argsort
     eval_q2m (metrics.py:124-157) on a bounded sample of the same workload."""
@@ -343,6 +372,7 @@ def main():
         if world == 1 and not args.no_extras:
             out["msrvtt1kA"] = msrvtt1ka()
             out["inference_topk"] = inference_leg()
+            out.update(other_configs_leg())
             if not args.no_cpu_baseline:
                 g_np = gallery.cpu().numpy()
                 q_np = q_local.cpu().numpy()

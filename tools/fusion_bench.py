@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--nv", type=int, default=44493)
     ap.add_argument("--chunk", type=int, default=8192, help="rows per combine_batches call (multiple of 32)")
     ap.add_argument("--loop-q", type=int, default=2048, help="queries timed through the per-batch loop")
-    a = ap.parse_args()
+    print(json.dumps(run(ap.parse_args())))
+
+
+def run(a):
+    """The C4 measurement for argparse-like `a` (nq, nv, chunk, loop_q): returns the JSON dict."""
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     m = Combiner(640, 2560, 5120).to(dev).eval()
@@ -96,7 +100,7 @@ def main():
                                               for k in (1, 5, 10, 50)]}
     total = dt_c + dt_r
     out["end_to_end"] = {"ms": total * 1e3, "queries_per_s": a.nq / total}
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
