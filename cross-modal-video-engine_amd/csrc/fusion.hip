@@ -17,6 +17,48 @@
 
 namespace cmve {
 
+// One row of LayerNorm held in registers as float4 runs (d <= 1024, d % 4 == 0, 16-byte aligned
+// rows): lane owns elements 4j .. 4j+3 for j = lane + 64 m.  fp64 statistics (biased variance, as
+// nn.LayerNorm); the per-lane summation order is fixed by this mapping, so layernorm_kernel and
+// layernorm_pack_kernel (which both call it) agree bit for bit.  emit(j, y0..y3) stores run j.
+template <typename Emit>
+__device__ __forceinline__ void ln_row_vec4(const float* __restrict__ xr, int d, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, double eps, Emit emit) {
+  const int lane = threadIdx.x & 63;
+  const int nv = d >> 2;
+  float4 v[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    v[m] = (lane + 64 * m < nv) ? reinterpret_cast<const float4*>(xr)[lane + 64 * m] : make_float4(0.f, 0.f, 0.f, 0.f);
+  double s = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if (lane + 64 * m < nv) s = (((s + (double)v[m].x) + (double)v[m].y) + (double)v[m].z) + (double)v[m].w;
+  const double mean = wave_sum(s) / (double)d;
+  double q = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if (lane + 64 * m < nv) {
+      const double c0 = (double)v[m].x - mean, c1 = (double)v[m].y - mean;
+      const double c2 = (double)v[m].z - mean, c3 = (double)v[m].w - mean;
+      q = fma(c3, c3, fma(c2, c2, fma(c1, c1, fma(c0, c0, q))));
+    }
+  const double rstd = 1.0 / sqrt(wave_sum(q) / (double)d + eps);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = lane + 64 * m;
+    if (j < nv) {
+      const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[j] : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 b = beta ? reinterpret_cast<const float4*>(beta)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      emit(j, (float)((((double)v[m].x - mean) * rstd) * (double)g.x + (double)b.x),
+           (float)((((double)v[m].y - mean) * rstd) * (double)g.y + (double)b.y),
+           (float)((((double)v[m].z - mean) * rstd) * (double)g.z + (double)b.z),
+           (float)((((double)v[m].w - mean) * rstd) * (double)g.w + (double)b.w));
+    }
+  }
+}
+
+template <bool VEC4>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx, int64_t n,
                                                         int64_t d, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, double eps,
@@ -25,6 +67,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const float* xr = x + row * ldx;
+  if constexpr (VEC4) {
+    float* yr = y + row * ldy;
+    ln_row_vec4(xr, (int)d, gamma, beta, eps, [&](int j, float a, float b, float c, float e) {
+      reinterpret_cast<float4*>(yr)[j] = make_float4(a, b, c, e);
+    });
+    return;
+  }
   if (d <= 1024) {  // the row read once into registers (16 per lane); same per-lane order as below
     float v[16];
 #pragma unroll
@@ -232,7 +281,10 @@ constexpr int TB_MAX = 12288;  // R * C floats staged per block (48 KiB + paddin
 // kv_d-float runs u are the raw p_s_m.reshape(G, T, gs, d) rows (g, t, bb) = (u / (T gs),
 // (u / gs) % T, u % gs); run u is written to row t*kvB + g*gs + bb -- the key/value order of
 // combiner.py:164-165 for G consecutive batches of gs rows (G = 1: the plain reshape).
-template <bool OUT_PACK>
+// V = 4: float4 block loads (C % 4 == 0) and four consecutive outputs of one row per thread
+// (row width % 4 == 0; a kv run then holds all four) -- one index computation per four elements and
+// 16-byte fp32 / 8-byte bf16 stores; V = 1 is the scalar form for the other shapes.
+template <bool OUT_PACK, int V>
 __global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ x, int64_t nb, int R, int C,
                                                       float* __restrict__ y, uint16_t* __restrict__ hi,
                                                       uint16_t* __restrict__ lo, int64_t d_pad, int kv_d = 0,
@@ -241,20 +293,46 @@ __global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ 
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
   const int W = R * C;
+  const int S = C + 1;
   if (b < nb) {
     const float* xb = x + b * (int64_t)W;
-    for (int e = tid; e < W; e += 256) tb[(e / C) * (C + 1) + (e % C)] = xb[e];
+    if constexpr (V == 4) {
+      for (int e4 = tid; e4 < (W >> 2); e4 += 256) {
+        const float4 v = reinterpret_cast<const float4*>(xb)[e4];
+        const int r = (e4 << 2) / C, c = (e4 << 2) - r * C;
+        float* t = tb + r * S + c;
+        t[0] = v.x;
+        t[1] = v.y;
+        t[2] = v.z;
+        t[3] = v.w;
+      }
+    } else {
+      for (int e = tid; e < W; e += 256) tb[(e / C) * S + (e % C)] = xb[e];
+    }
     __syncthreads();
   }
   const int ow = OUT_PACK ? (int)d_pad : R;  // output row width
-  for (int e = tid; e < C * ow; e += 256) {
-    const int c = e / ow, k = e - c * ow;
-    const float v = (b < nb && k < R) ? tb[k * (C + 1) + c] : 0.f;
+  const int owv = ow / V;
+  for (int ev = tid; ev < C * owv; ev += 256) {
+    const int c = ev / owv, k = (ev - c * owv) * V;
+    float v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = (b < nb && k + j < R) ? tb[(k + j) * S + c] : 0.f;
     int64_t o = (b * C + c) * (int64_t)ow + k;
     if constexpr (OUT_PACK) {
-      const uint16_t h = f2bf(v);
-      hi[o] = h;
-      lo[o] = f2bf(v - bf2f(h));
+      uint16_t hh[V], ll[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        hh[j] = f2bf(v[j]);
+        ll[j] = f2bf(v[j] - bf2f(hh[j]));
+      }
+      if constexpr (V == 4) {
+        reinterpret_cast<uint2*>(hi + o)[0] = make_uint2(hh[0] | ((uint32_t)hh[1] << 16), hh[2] | ((uint32_t)hh[3] << 16));
+        reinterpret_cast<uint2*>(lo + o)[0] = make_uint2(ll[0] | ((uint32_t)ll[1] << 16), ll[2] | ((uint32_t)ll[3] << 16));
+      } else {
+        hi[o] = hh[0];
+        lo[o] = ll[0];
+      }
     } else {
       if (kv_d > 0) {  // 32-bit index math (the host checks nb * R * C < 2^32)
         const uint32_t ou = (uint32_t)o, u = ou / (uint32_t)kv_d, w = ou - u * (uint32_t)kv_d;
@@ -262,13 +340,17 @@ __global__ __launch_bounds__(256) void tblocks_kernel(const float* __restrict__ 
         const uint32_t t = rem / (uint32_t)kv_gs, bb = rem - t * (uint32_t)kv_gs;
         o = ((int64_t)t * kv_B + (int64_t)g * kv_gs + bb) * kv_d + w;
       }
-      y[o] = v;
+      if constexpr (V == 4)
+        reinterpret_cast<float4*>(y + o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      else
+        y[o] = v[0];
     }
   }
 }
 
 // LayerNorm of rows of x (the register-row path of layernorm_kernel, same arithmetic) written as
 // the split-bf16 planes of a raw GEMM operand; rows [n, n_pad) and columns [d, d_pad) are zero.
+template <bool VEC4>
 __global__ __launch_bounds__(256) void layernorm_pack_kernel(const float* __restrict__ x, int64_t ldx, int64_t n,
                                                              int64_t d, int64_t n_pad, int64_t d_pad,
                                                              const float* __restrict__ gamma,
@@ -284,6 +366,18 @@ __global__ __launch_bounds__(256) void layernorm_pack_kernel(const float* __rest
     return;
   }
   const float* xr = x + row * ldx;
+  if constexpr (VEC4) {  // d_pad % 4 == 0: four bf16 per 8-byte store
+    ln_row_vec4(xr, (int)d, gamma, beta, eps, [&](int j, float a, float b, float c, float e) {
+      const uint16_t h0 = f2bf(a), h1 = f2bf(b), h2 = f2bf(c), h3 = f2bf(e);
+      reinterpret_cast<uint2*>(hr)[j] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+      reinterpret_cast<uint2*>(lr)[j] =
+          make_uint2(f2bf(a - bf2f(h0)) | ((uint32_t)f2bf(b - bf2f(h1)) << 16),
+                     f2bf(c - bf2f(h2)) | ((uint32_t)f2bf(e - bf2f(h3)) << 16));
+    });
+    for (int64_t j = (d >> 2) + lane; j < (d_pad >> 2); j += 64)
+      reinterpret_cast<uint2*>(hr)[j] = reinterpret_cast<uint2*>(lr)[j] = make_uint2(0u, 0u);
+    return;
+  }
   float v[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) v[m] = (lane + 64 * m < d) ? xr[lane + 64 * m] : 0.f;
@@ -318,13 +412,27 @@ __global__ __launch_bounds__(256) void layernorm_pack_kernel(const float* __rest
 
 using namespace cmve;
 
+static bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// tblocks_kernel<., 4>: float4 block loads (C % 4 == 0, 16-byte x) and output rows of ow % 4 == 0
+static bool tb_vec4(const float* x, int64_t C, int64_t ow) { return C % 4 == 0 && ow % 4 == 0 && a16(x); }
+
+// float4 rows for ln_row_vec4: d <= 1024 and every row / gamma / beta 16-byte aligned
+static bool ln_vec4_ok(const float* x, int64_t ldx, int64_t d, const float* gamma, const float* beta) {
+  return d <= 1024 && d % 4 == 0 && ldx % 4 == 0 && a16(x) && (!gamma || a16(gamma)) && (!beta || a16(beta));
+}
+
 extern "C" int cmve_layernorm(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, const float* gamma,
                               const float* beta, double eps, float* y, int64_t ldy) {
   CMVE_REQUIRE(h && x && y, "cmve_layernorm: NULL argument");
   CMVE_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldy >= d, "cmve_layernorm: bad shape");
   if (n == 0) return CMVE_OK;
-  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream, x, ldx, n, d, gamma,
-                     beta, eps, y, ldy);
+  if (ln_vec4_ok(x, ldx, d, gamma, beta) && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0)
+    hipLaunchKernelGGL(layernorm_kernel<true>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream, x, ldx, n, d,
+                       gamma, beta, eps, y, ldy);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<false>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream, x, ldx, n, d,
+                       gamma, beta, eps, y, ldy);
   return check_launch("layernorm");
 }
 
@@ -377,8 +485,12 @@ extern "C" int cmve_transpose_blocks(cmve_handle_t h, const float* x, int64_t nb
                "cmve_transpose_blocks: bad block shape");
   if (nb == 0) return CMVE_OK;
   const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
-  hipLaunchKernelGGL(tblocks_kernel<false>, dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R, (int)C, y,
-                     nullptr, nullptr, (int64_t)0);
+  if (tb_vec4(x, C, R) && a16(y))
+    hipLaunchKernelGGL((tblocks_kernel<false, 4>), dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R,
+                       (int)C, y, nullptr, nullptr, (int64_t)0);
+  else
+    hipLaunchKernelGGL((tblocks_kernel<false, 1>), dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R,
+                       (int)C, y, nullptr, nullptr, (int64_t)0);
   return check_launch("transpose_blocks");
 }
 
@@ -392,8 +504,12 @@ extern "C" int cmve_transpose_blocks_kv(cmve_handle_t h, const float* x, int64_t
   CMVE_REQUIRE(nb * R * C < (1ll << 32), "cmve_transpose_blocks_kv: more than 2^32 elements (split the batch)");
   if (nb == 0) return CMVE_OK;
   const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
-  hipLaunchKernelGGL(tblocks_kernel<false>, dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R, (int)C, y,
-                     nullptr, nullptr, (int64_t)0, (int)d, (int)T, (int)gs, (int)B);
+  if (tb_vec4(x, C, R) && d % 4 == 0 && a16(y))
+    hipLaunchKernelGGL((tblocks_kernel<false, 4>), dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R,
+                       (int)C, y, nullptr, nullptr, (int64_t)0, (int)d, (int)T, (int)gs, (int)B);
+  else
+    hipLaunchKernelGGL((tblocks_kernel<false, 1>), dim3((unsigned)nb), dim3(256), lds, h->stream, x, nb, (int)R,
+                       (int)C, y, nullptr, nullptr, (int64_t)0, (int)d, (int)T, (int)gs, (int)B);
   return check_launch("transpose_blocks_kv");
 }
 
@@ -406,8 +522,12 @@ extern "C" int cmve_pack_tblocks(cmve_handle_t h, const float* x, int64_t nb, in
   const size_t lds = sizeof(float) * (size_t)R * (size_t)(C + 1);
   const int64_t grid = out->n_pad / C;  // blocks past nb write the zero padding rows
   if (grid) {
-    hipLaunchKernelGGL(tblocks_kernel<true>, dim3((unsigned)grid), dim3(256), lds, h->stream, x, nb, (int)R, (int)C,
-                       nullptr, out->hi, out->lo, out->d_pad);
+    if (tb_vec4(x, C, out->d_pad) && ((uintptr_t)out->hi & 7) == 0 && ((uintptr_t)out->lo & 7) == 0)
+      hipLaunchKernelGGL((tblocks_kernel<true, 4>), dim3((unsigned)grid), dim3(256), lds, h->stream, x, nb, (int)R,
+                         (int)C, nullptr, out->hi, out->lo, out->d_pad);
+    else
+      hipLaunchKernelGGL((tblocks_kernel<true, 1>), dim3((unsigned)grid), dim3(256), lds, h->stream, x, nb, (int)R,
+                         (int)C, nullptr, out->hi, out->lo, out->d_pad);
     int st = check_launch("pack_tblocks");
     if (st) return st;
   }
@@ -420,8 +540,13 @@ extern "C" int cmve_layernorm_pack(cmve_handle_t h, const float* x, int64_t ldx,
   CMVE_REQUIRE(n >= 0 && d > 0 && d <= 1024 && ldx >= d, "cmve_layernorm_pack: bad shape (d <= 1024)");
   CMVE_REQUIRE(out->n == n && out->d == d && out->d_pad >= d && out->n_pad >= n, "cmve_layernorm_pack: bad out");
   if (out->n_pad) {
-    hipLaunchKernelGGL(layernorm_pack_kernel, dim3((unsigned)((out->n_pad + 3) / 4)), dim3(256), 0, h->stream, x,
-                       ldx, n, d, out->n_pad, out->d_pad, gamma, beta, eps, out->hi, out->lo);
+    if (ln_vec4_ok(x, ldx, d, gamma, beta) && out->d_pad % 4 == 0 && ((uintptr_t)out->hi & 7) == 0 &&
+        ((uintptr_t)out->lo & 7) == 0)
+      hipLaunchKernelGGL(layernorm_pack_kernel<true>, dim3((unsigned)((out->n_pad + 3) / 4)), dim3(256), 0, h->stream,
+                         x, ldx, n, d, out->n_pad, out->d_pad, gamma, beta, eps, out->hi, out->lo);
+    else
+      hipLaunchKernelGGL(layernorm_pack_kernel<false>, dim3((unsigned)((out->n_pad + 3) / 4)), dim3(256), 0,
+                         h->stream, x, ldx, n, d, out->n_pad, out->d_pad, gamma, beta, eps, out->hi, out->lo);
     int st = check_launch("layernorm_pack");
     if (st) return st;
   }

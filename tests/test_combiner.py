@@ -96,3 +96,51 @@ def test_gpu_fused_transpose_and_layernorm_packing():
     pk = engine.PackedOperand.layernorm(z, ln.weight, ln.bias, ln.eps)
     rz = engine.RowSet(_layernorm(z, ln), with_lo=True, with_f16=False, raw_rows=True)
     assert torch.equal(pk.hi, rz.hi) and torch.equal(pk.lo, rz.lo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,strided", [(640, False), (200, True), (201, False), (1024, False), (1500, False)])
+def test_gpu_layernorm_paths(d, strided):
+    """cmve_layernorm (float4 rows when d % 4 == 0 and the rows are aligned, else the scalar rows)
+    against an fp64 LayerNorm, and cmve_layernorm_pack equal to packing its output, bit for bit."""
+    import torch
+    from cmve import engine
+    from cmve.multifusion.combiner import _layernorm
+    rng = np.random.default_rng(d)
+    ln = torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    base = torch.from_numpy((3 * rng.standard_normal((517, d + 8)) + 1).astype(np.float32)).cuda()
+    z = base[:, :d].contiguous()
+    y = _layernorm(z, ln)
+    if strided:  # rows at a 4-byte offset with ldx = d + 8: the scalar-row kernel on the same values
+        from cmve._lib import lib
+        zs = base[:, 1:1 + d]
+        zs.copy_(z)
+        ys = torch.empty_like(z)
+        assert lib.cmve_layernorm(engine.handle(z.device), engine._ptr(zs), zs.stride(0), zs.shape[0], d,
+                                  engine._ptr(ln.weight.detach()), engine._ptr(ln.bias.detach()), float(ln.eps),
+                                  engine._ptr(ys), ys.stride(0)) == 0
+        assert (ys - y).abs().max().item() < 1e-6
+    z64 = z.double()
+    ref = torch.nn.functional.layer_norm(z64, (d,), ln.weight.double(), ln.bias.double(), ln.eps)
+    assert (y.double() - ref).abs().max().item() < 2e-6
+    if d <= 1024:
+        pk = engine.PackedOperand.layernorm(z, ln.weight, ln.bias, ln.eps)
+        rz = engine.RowSet(y, with_lo=True, with_f16=False, raw_rows=True)
+        assert torch.equal(pk.hi, rz.hi) and torch.equal(pk.lo, rz.lo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,C", [(5, 7), (16, 12), (12, 16)])
+def test_gpu_transpose_blocks_shapes(R, C):
+    """Block transposes on the scalar (C or R not a multiple of 4) and float4 forms, against torch."""
+    import torch
+    from cmve import engine
+    y = torch.randn(9 * R * C, generator=torch.Generator().manual_seed(R * C)).cuda()
+    ref = y.view(9, R, C).transpose(1, 2).reshape(9 * C, R)
+    assert torch.equal(engine.transpose_blocks(y, R, C), ref)
+    op = engine.PackedOperand.from_blocks_transposed(y.view(9, R, C), R, C)
+    rs = engine.RowSet(ref.contiguous(), with_lo=True, with_f16=False, raw_rows=True)
+    assert torch.equal(op.hi[:rs.n_pad], rs.hi) and torch.equal(op.lo[:rs.n_pad], rs.lo)
