@@ -4,6 +4,7 @@
 //   EPI_RANK   : per-row and per-column "score > threshold" counts + undecided-pair list
 //                (the GT rank of LINAS-engine/util/metrics.py:137-147 without the matrix)
 //   EPI_LINEAR : BN(resid + act(x.w + bias))               (MFC / Combiner projections)
+//   EPI_BIAS   : x.w + bias (+ ReLU): EPI_LINEAR's common case as its own instantiation
 //   EPI_TOPK   : the RANK epilogue with thresholds (+inf, tau): every s >= tau emitted as a
 //                (score key, row, column) entry, bucketed by 256-row QUERY tile (topk.hip K13)
 //
@@ -29,7 +30,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int BK = 64;
-constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2, EPI_TOPK = 3;
+constexpr int EPI_STORE = 0, EPI_RANK = 1, EPI_LINEAR = 2, EPI_TOPK = 3, EPI_BIAS = 4;
 // epilogues that count / emit against per-row and per-column thresholds
 constexpr bool epi_thr(int e) { return e == EPI_RANK || e == EPI_TOPK; }
 
@@ -273,6 +274,23 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       lo = a.col_lo[no + tid - BM];
     }
   };
+  // EPI_BIAS / EPI_LINEAR: the tile's bias (and BN) columns are fetched with its loads too
+  constexpr bool EPI_COLS = EPI == EPI_BIAS || EPI == EPI_LINEAR;
+  constexpr int NCV = EPI == EPI_LINEAR ? 3 : 1;  // bias, bn_scale, bn_shift
+  float colv[NCV][TN];
+  auto fetch_cols = [&](int no, float (*cv)[TN]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = no + wc * (TN * 16) + j * 16 + (lane & 15);
+      const bool ok = col < a.ng;
+      cv[0][j] = (a.bias && ok) ? a.bias[col] : 0.f;
+      if constexpr (NCV == 3) {
+        cv[1][j] = (a.bn_scale && ok) ? a.bn_scale[col] : 1.f;
+        cv[2][j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
+      }
+    }
+  };
+  if constexpr (EPI_COLS) fetch_cols(n0, colv);
   if constexpr (epi_thr(EPI)) {
     static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
@@ -313,16 +331,30 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     const int rbase = m0 + wr * (TM * 16) + (lane >> 4) * 4;
     const int cbase = n0 + wc * (TN * 16) + (lane & 15);
 
-    if constexpr (EPI == EPI_LINEAR) {
-      float bj[TN], sj[TN], hj[TN];
+    if constexpr (EPI == EPI_BIAS) {
+      // bias (+ ReLU) only: a separate instantiation, so the general form's act / resid / BN
+      // arguments do not hold scalar registers through the main loop (that one spills SGPRs), and
+      // the bias columns arrive with the tile's loads (bias_v) instead of an HBM wait in here,
+      // which would also wait for the next tile's staging loads already in flight
+      const bool relu = a.relu == 1;
+      float* outp = (float*)a.out;
   #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = cbase + j * 16;
-        const bool ok = col < a.ng;
-        bj[j] = (a.bias && ok) ? a.bias[col] : 0.f;
-        sj[j] = (a.bn_scale && ok) ? a.bn_scale[col] : 1.f;
-        hj[j] = (a.bn_shift && ok) ? a.bn_shift[col] : 0.f;
-      }
+      for (int i = 0; i < TM; ++i)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + i * 16 + r;
+          if (row >= a.nq) continue;
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = cbase + j * 16;
+            const float v = acc[i][j][r] + colv[0][j];
+            if (col < a.ng) outp[(int64_t)row * a.ldo + col] = relu ? fmaxf(v, 0.f) : v;
+          }
+        }
+    } else if constexpr (EPI == EPI_LINEAR) {
+      const float* bj = colv[0];
+      const float* sj = colv[NCV - 1 > 0 ? 1 : 0];
+      const float* hj = colv[NCV - 1 > 0 ? 2 : 0];
   #pragma unroll
       for (int i = 0; i < TM; ++i)
   #pragma unroll
@@ -713,6 +745,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     const bool has_next = next < ntiles;
     int m0n = 0, n0n = 0;
     float thn_hi = 0.f, thn_lo = 0.f;
+    float coln[NCV][TN];
     if (has_next) {
       tile_origin(next, m0n, n0n);
       rA = rsrc_of(a.qhi, m0n, BM);
@@ -723,9 +756,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       }
       prologue_loads();
       if constexpr (epi_thr(EPI)) fetch_thr(m0n, n0n, thn_hi, thn_lo);
+      if constexpr (EPI_COLS) fetch_cols(n0n, coln);
     }
     epilogue();
     if (!has_next) break;
+    if constexpr (EPI_COLS)
+#pragma unroll
+      for (int c = 0; c < NCV; ++c)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) colv[c][j] = coln[c][j];
     tile = next;
     m0 = m0n;
     n0 = n0n;
@@ -1162,5 +1201,6 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
   a.resid = resid;
   a.ldr = ldr;
   a.relu = relu;
+  if (!resid && !bn_scale && relu <= 1) return dispatch<EPI_BIAS>(a, x, w, mode, h->stream);
   return dispatch<EPI_LINEAR>(a, x, w, mode, h->stream);
 }
