@@ -25,6 +25,8 @@ DIR_ROW, DIR_COL = 1, 2
 ROW_ALIGN, DIM_ALIGN = 256, 64
 TOPK_MAX = 2048
 MAX_CHUNKS = 16
+EVAL_TIMING_SLOTS = 32
+EVAL_OUT_HEAD = 16
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD = 0, 1, 2, 3, 4
@@ -77,6 +79,11 @@ SIGNATURES = {
                                           _vp, _vp, _i64, _vp, _i32]),
     "cmve_overlap_mfma_ms": (C.c_int, [_vp, _P(_f32), _P(_i32)]),
     "cmve_rank_thresholds": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp]),
+    "cmve_gt_ranks": (C.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _vp]),
+    "cmve_eval_workspace": (C.c_int, [_P(Rows), _P(Rows), _i64, _P(_i64)]),
+    "cmve_eval_ranks": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i32]),
+    "cmve_eval_timing": (C.c_int, [_vp, _i32, _P(_f32)]),
+    "cmve_merge_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_topk_workspace": (C.c_int, [_P(Rows), _P(Rows), _i32, _P(_i64)]),
@@ -114,7 +121,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

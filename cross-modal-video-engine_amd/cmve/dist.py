@@ -43,13 +43,29 @@ def local_gt_lists(gts_global: Sequence[Sequence[int]], lo: int, hi: int):
     return [[g - lo for g in l if lo <= g < hi] for l in gts_global]
 
 
+_NAN_GT = -1e300  # below every cosine: "this shard's GTs all score NaN" inside the MAX all-reduce
+
+
+def encode_gt_scores(sgt: torch.Tensor) -> torch.Tensor:
+    """Per-shard GT scores (cmve_gt_thresholds: NaN = no GT in this shard, +inf = GTs here but every
+    one scores NaN, else the best finite score) -> keys whose MAX over the shards is the global
+    answer: a finite score wins over NaN GTs, which win over no GT (NaN -> -inf, +inf -> -1e300)."""
+    return torch.nan_to_num(sgt, nan=-np.inf, posinf=_NAN_GT)
+
+
+def decode_gt_scores(key: torch.Tensor) -> torch.Tensor:
+    """Inverse of encode_gt_scores after the MAX: -inf -> NaN (no GT anywhere), -1e300 -> +inf."""
+    s = torch.where(key == _NAN_GT, torch.full_like(key, float("inf")), key)
+    return torch.where(torch.isinf(s) & (s < 0), torch.full_like(s, float("nan")), s)
+
+
 def merge_gt_scores(sgt_partial: torch.Tensor, world: int) -> torch.Tensor:
-    """all-reduce(MAX) of per-shard best-GT scores; NaN (no GT in this shard) -> -inf -> NaN."""
+    """all-reduce(MAX) of per-shard best-GT scores (encode / MAX / decode)."""
     if world == 1:
         return sgt_partial
-    s = torch.nan_to_num(sgt_partial, nan=-np.inf)
+    s = encode_gt_scores(sgt_partial)
     dist.all_reduce(s, op=dist.ReduceOp.MAX)
-    return torch.where(torch.isinf(s) & (s < 0), torch.full_like(s, float('nan')), s)
+    return decode_gt_scores(s)
 
 
 def reduce_counts(cnt: torch.Tensor, world: int) -> torch.Tensor:
@@ -78,9 +94,9 @@ def any_flag(flag: torch.Tensor, world: int) -> torch.Tensor:
 
 
 def ranks_from(cnt: torch.Tensor, sgt: torch.Tensor, n_q: int, n_global: int) -> torch.Tensor:
-    no_gt = torch.isnan(sgt[:n_q])
-    c = cnt[:n_q].to(torch.int64)
-    return torch.where(no_gt, torch.full_like(c, n_global + 1), c + 1)
+    """Global 1-based ranks on the device (cmve_gt_ranks): no GT (NaN) -> n_global + 1, every GT NaN
+    (+inf) -> n_global, else count + 1."""
+    return engine.gt_ranks(cnt, sgt, n_q, n_global)
 
 
 def pad_topk(idx: torch.Tensor, scores: torch.Tensor, k: int):
@@ -93,41 +109,46 @@ def pad_topk(idx: torch.Tensor, scores: torch.Tensor, k: int):
     return torch.cat([idx, pi], 1), torch.cat([scores, ps], 1)
 
 
+def gather_topk(idx_global: torch.Tensor, scores: torch.Tensor, world: int):
+    """all-gather of every shard's local top-k: [n_q, world * k] ids (int64) / fp64 scores, shard r's
+    run at columns [r*k, (r+1)*k) of each query (the layout cmve_merge_topk reads)."""
+    ids = idx_global.to(torch.int64).contiguous()
+    sc = scores.to(torch.float64).contiguous()
+    if world == 1:
+        return ids, sc
+    n_q, kk = ids.shape
+    gi = torch.empty((world * n_q, kk), dtype=ids.dtype, device=ids.device)
+    gs = torch.empty((world * n_q, kk), dtype=sc.dtype, device=sc.device)
+    dist.all_gather_into_tensor(gi, ids)
+    dist.all_gather_into_tensor(gs, sc)
+    return (gi.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1).contiguous(),
+            gs.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1).contiguous())
+
+
+def merge_sorted_topk(ids: torch.Tensor, scores: torch.Tensor, lists: int, k: int):
+    """cmve_merge_topk on the device: `lists` sorted runs per query -> the best k (score desc, global
+    id asc; empty slots -1 / NaN)."""
+    n_q, width = ids.shape
+    k_in = width // lists
+    out_i = torch.empty((n_q, k), dtype=torch.int64, device=ids.device)
+    out_s = torch.empty((n_q, k), dtype=torch.float64, device=ids.device)
+    _lib.check(_lib.lib.cmve_merge_topk(engine.handle(ids.device), engine._ptr(ids.contiguous()),
+                                        engine._ptr(scores.contiguous()), n_q, lists, k_in, k,
+                                        engine._ptr(out_i), engine._ptr(out_s)), "cmve_merge_topk")
+    return out_i, out_s
+
+
 def merge_topk(idx_global: torch.Tensor, scores: torch.Tensor, k: int, world: int, to_host: bool = True):
-    """Gather every shard's local top-k (global ids, fp64 scores) and keep the best k per query,
-    ordered (score desc, global id asc) -- on the device: a stable sort by id, then a stable sort by
-    descending score.  idx_global/scores: [n_q, k_local]; id -1 marks an empty slot (score ignored).
-    Returns (ids int64 [n_q, k'], scores fp64 [n_q, k']) with k' = min(k, world * k_local); slots
-    past the available entries hold -1 / NaN."""
-    n_q, kk = idx_global.shape
-    if world == 1:  # one shard: its top-k is already in (score desc, id asc) order
-        ids = idx_global.to(torch.int64)[:, :k]
-        sc = scores.to(torch.float64)[:, :k]
-        sc = torch.where(ids < 0, torch.full_like(sc, float("nan")), sc)
-        return (ids, sc) if not to_host else (ids.cpu().numpy(), sc.cpu().numpy())
-    if world > 1:
-        gi = torch.empty((world * n_q, kk), dtype=idx_global.dtype, device=idx_global.device)
-        gs = torch.empty((world * n_q, kk), dtype=scores.dtype, device=scores.device)
-        dist.all_gather_into_tensor(gi, idx_global.contiguous())
-        dist.all_gather_into_tensor(gs, scores.contiguous())
-        idx_global = gi.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
-        scores = gs.reshape(world, n_q, kk).permute(1, 0, 2).reshape(n_q, -1)
-    ids = idx_global.to(torch.int64)
-    sc = scores.to(torch.float64)
-    empty = ids < 0
-    key_id = torch.where(empty, torch.full_like(ids, torch.iinfo(torch.int64).max), ids)
-    key_sc = torch.where(empty, torch.full_like(sc, -float("inf")), sc)
-    o1 = torch.argsort(key_id, dim=1, stable=True)
-    key_id, key_sc, empty = key_id.gather(1, o1), key_sc.gather(1, o1), empty.gather(1, o1)
-    o2 = torch.argsort(-key_sc, dim=1, stable=True)
+    """Gather every shard's local top-k (global ids, fp64 scores; id -1 = empty slot) and keep the best
+    k per query, ordered (score desc, global id asc), by the HIP k-way merge.  Returns (ids int64
+    [n_q, k'], scores fp64 [n_q, k']), k' = min(k, world * k_local); slots past the available entries
+    hold -1 / NaN."""
+    ids, sc = gather_topk(idx_global, scores, world)
     kout = min(k, ids.shape[1])
-    o2 = o2[:, :kout]
-    out_id, out_sc, out_empty = key_id.gather(1, o2), key_sc.gather(1, o2), empty.gather(1, o2)
-    out_id = torch.where(out_empty, torch.full_like(out_id, -1), out_id)
-    out_sc = torch.where(out_empty, torch.full_like(out_sc, float("nan")), out_sc)
+    out_i, out_s = merge_sorted_topk(ids, sc, world, kout)
     if not to_host:
-        return out_id, out_sc
-    return out_id.cpu().numpy(), out_sc.cpu().numpy()
+        return out_i, out_s
+    return out_i.cpu().numpy(), out_s.cpu().numpy()
 
 
 class ShardedGallery:
@@ -160,23 +181,20 @@ class ShardedGallery:
         """Global 1-based GT ranks of all gathered queries (t2v direction).
 
         q_local: this rank's [n_local, D] query embeddings (equal n_local on every rank);
-        gt_csr: (off, idx) from ``local_gt_csr`` for the GATHERED query order."""
+        gt_csr: (off, idx) from ``local_gt_csr`` for the GATHERED query order.  The overflow flag of
+        the undecided-pair list rides the counts' all-reduce, so every rank sees the same flag: all of
+        them grow their lists and redo the batch together (a rank that trusted its own flag alone would
+        return incomplete counts while another waited in the next all-gather)."""
         q_all = self.all_gather_rows(q_local)
-        q = engine.RowSet(q_all, with_lo=(mode == _lib.SIM_BF16X3), with_f16=(mode == _lib.SIM_F16),
-                          device=self.device)
-        off, idx = gt_csr
-        sgt, _, _ = engine.gt_thresholds(q, self.shard, off, idx, mode)
-        sgt = merge_gt_scores(sgt, self.world)
-        hi, lo = engine.rank_thresholds(q, self.shard, sgt, mode)
-        cnt, _ = engine.rank_count_launch(q, self.shard, mode, row=(sgt, hi, lo), ws=self.ws, events=events,
-                                          chunks=chunks)
-        cnt = reduce_counts(cnt, self.world)
-        ranks = ranks_from(cnt, sgt, n_q, self.n_global)
+        for _attempt in range(4):
+            ranks, ovf = self.rank_queries_device(q_all, gt_csr, n_q, mode, events, chunks)
+            if not bool(ovf.item()):
+                break
+            self.ws.grow()  # every rank: the flag is the all-reduced one
+        else:
+            raise _lib.CmveError("ShardedGallery.rank_queries: undecided-pair list kept overflowing")
         if not return_host:
             return ranks
-        if self.ws.overflowed():  # overflow: grow and redo (correctness first)
-            self.ws.grow()
-            return self.rank_queries(q_local, gt_csr, n_q, mode, None, return_host, chunks)
         return ranks.cpu().numpy().astype(np.int64)
 
     def gather_rows_async(self, x_local: torch.Tensor, out: torch.Tensor):
@@ -210,10 +228,14 @@ class ShardedGallery:
         q_all = self.all_gather_rows(q_local)
         q = engine.RowSet(q_all, with_lo=self.shard.has_lo, with_f16=self.shard.has_f16, device=self.device)
         kk = min(k, self.shard.n)
-        idx, sc = engine.topk(q, self.shard, kk, mode=mode, to_host=False)
-        idx = idx.to(torch.int64)
-        idx = torch.where(idx >= 0, idx + self.offset, idx)
-        idx, sc = pad_topk(idx, sc, k)  # every rank contributes k columns (shards may hold fewer rows)
+        if kk < 1:  # an empty shard (shard_bounds' last rank): contributes k empty slots
+            idx = torch.full((q.n, k), -1, dtype=torch.int64, device=self.device)
+            sc = torch.full((q.n, k), float("nan"), dtype=torch.float64, device=self.device)
+        else:
+            idx, sc = engine.topk(q, self.shard, kk, mode=mode, to_host=False)
+            idx = idx.to(torch.int64)
+            idx = torch.where(idx >= 0, idx + self.offset, idx)
+            idx, sc = pad_topk(idx, sc, k)  # every rank contributes k columns (shards may hold fewer rows)
         return merge_topk(idx, sc, k, self.world)
 
 

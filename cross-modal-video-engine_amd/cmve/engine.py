@@ -372,133 +372,117 @@ def gt_rank_counts(q: RowSet, g: RowSet, row_gts=None, col_gts=None, mode: int =
         ws.grow(ncand)
     else:
         raise _lib.CmveError("rank_count: candidate list kept overflowing")
-    out_r = out_c = None
-    if row_gts is not None:
-        out_r = rc[:q.n].to(torch.int64).cpu().numpy() + 1
-        empty = np.fromiter((len(l) == 0 for l in row_gts), bool, count=len(row_gts))
-        out_r[empty] = g.n + 1
-    if col_gts is not None:
-        out_c = cc[:g.n].to(torch.int64).cpu().numpy() + 1
-        empty = np.fromiter((len(l) == 0 for l in col_gts), bool, count=len(col_gts))
-        out_c[empty] = q.n + 1
+    out_r = gt_ranks(rc, row[0], q.n, g.n).cpu().numpy() if row_gts is not None else None
+    out_c = gt_ranks(cc, col[0], g.n, q.n).cpu().numpy() if col_gts is not None else None
     return out_r, out_c, ncand
+
+
+def gt_ranks(cnt: torch.Tensor, sgt: torch.Tensor, n: int, n_m: int, out: Optional[torch.Tensor] = None,
+             recall: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """1-based ranks int64 [n] on the device from better-than-GT counts and GT scores (cmve_gt_ranks):
+    empty GT list (sgt NaN) -> n_m + 1, every GT NaN (sgt +inf) -> n_m, else count + 1
+    (``LINAS-engine/util/metrics.py:137-147``).  recall: optional int64 [4] device output
+    (#rank<=1, #rank<=5, #rank<=10, sum of ranks)."""
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=cnt.device)
+    check(lib.cmve_gt_ranks(handle(cnt.device), _ptr(cnt), _ptr(sgt), n, n_m, _ptr(out), _ptr(recall)),
+          "cmve_gt_ranks")
+    return out[:n]
 
 
 class RankSession:
     """Resident exact GT-rank evaluation of a fixed problem (the reference re-runs
     ``encode_* -> cal_error -> cal_perf`` on new embeddings of the same sets every validation,
-    ``LINAS-engine/validate.py:61-74``): raw / packed buffers of both sets, the GT lists, thresholds,
-    counts and the undecided-pair list are allocated once, and one evaluation -- pack both sets,
-    GT scores and thresholds of both directions, the fused rank GEMM, the fp64 fix-up, ranks --
-    is enqueued on a stream of its own.  ``run(captions, videos)`` copies the new embeddings in and
-    returns (t2v ranks, v2t ranks) as ``gt_rank_counts`` does, bit for bit.  An undecided-pair
-    overflow (checked after every run) grows the list and redoes the run.
-    graph=True captures the evaluation into one hipGraph.  Its replays raced with a device-to-device
-    input copy ordered only by a stream wait (garbage pair counts after a few replays on the MI355X
-    box), so a replay first synchronises the device; measured 0.22 ms per C1 evaluation against
-    0.19 ms for the eager enqueue, hence graph=False by default."""
+    ``LINAS-engine/validate.py:61-74``): the packed planes of both sets, the GT lists, thresholds,
+    counts and the undecided-pair list are allocated once, and one evaluation is THREE launches on
+    the caller's current stream (``cmve_eval_ranks``, K14): pack both sets + exact GT scores +
+    thresholds, the fused rank GEMM, the fp64 fix-up + ranks + R@K sums.
+    ``run(captions, videos)`` returns (t2v ranks, v2t ranks) exactly as ``gt_rank_counts`` does.
+    Device tensors of the session's dtype are read in place (no copy); anything else is copied into
+    the session's own buffers first.  An undecided-pair overflow grows the list and redoes the run.
+    ``enqueue`` + ``stats`` is the non-blocking form (R@K sums / overflow on the device)."""
 
     def __init__(self, n_q: int, n_g: int, d: int, row_gts=None, col_gts=None, dtype=torch.float32,
                  mode: int = _lib.SIM_F16, eps: float = 0.0, device: Optional[torch.device] = None,
-                 graph: bool = False):
+                 cand_cap: Optional[int] = None):
         if row_gts is None and col_gts is None:
             raise ValueError("RankSession: need row_gts and/or col_gts")
+        if n_q < 1 or n_g < 1:
+            raise ValueError("RankSession: both sets need rows")
         self.device = device or default_device()
         dev = self.device
-        self.mode, self.graph = mode, graph
+        self.mode, self.dtype = mode, dtype
         self.q = RowSet(torch.zeros((n_q, d), dtype=dtype, device=dev), eps=eps, with_lo=(mode == _lib.SIM_BF16X3),
                         with_f16=(mode == _lib.SIM_F16), device=dev)
         self.g = RowSet(torch.zeros((n_g, d), dtype=dtype, device=dev), eps=eps, with_lo=(mode == _lib.SIM_BF16X3),
                         with_f16=(mode == _lib.SIM_F16), device=dev)
-        self.row = self.col = None
-        if row_gts is not None:
-            off, idx = csr(row_gts, dev)
-            self.row = (off, idx) + tuple(torch.empty(self.q.n_pad, dtype=t, device=dev)
-                                          for t in (torch.float64, torch.float32, torch.float32))
-            self.row_cnt = torch.zeros(self.q.n_pad, dtype=torch.int32, device=dev)
-            self.row_empty = torch.from_numpy(np.fromiter((len(l) == 0 for l in row_gts), bool,
-                                                          count=len(row_gts))).to(dev)
-        if col_gts is not None:
-            off, idx = csr(col_gts, dev)
-            self.col = (off, idx) + tuple(torch.empty(self.g.n_pad, dtype=t, device=dev)
-                                          for t in (torch.float64, torch.float32, torch.float32))
-            self.col_cnt = torch.zeros(self.g.n_pad, dtype=torch.int32, device=dev)
-            self.col_empty = torch.from_numpy(np.fromiter((len(l) == 0 for l in col_gts), bool,
-                                                          count=len(col_gts))).to(dev)
-        self.ws = RankWorkspace(dev, cap=max(1 << 16, 64 * (n_q + n_g)))
-        self.out = torch.zeros(n_q + n_g + 1, dtype=torch.int64, device=dev)  # t2v | v2t | pair count
-        self.host = torch.zeros(n_q + n_g + 1, dtype=torch.int64).pin_memory()
-        self._graph = None
-        self._stream = torch.cuda.Stream(dev)
-        self._warm = 0
+        self.row = csr(row_gts, dev) if row_gts is not None else None
+        self.col = csr(col_gts, dev) if col_gts is not None else None
+        self._alloc(int(cand_cap) if cand_cap else max(1 << 16, 64 * (n_q + n_g)))
+        self.out = torch.zeros(_lib.EVAL_OUT_HEAD + n_q + n_g, dtype=torch.int64, device=dev)
+        self.host = torch.zeros(_lib.EVAL_OUT_HEAD + n_q + n_g, dtype=torch.int64).pin_memory()
+        self._bound = (None, None)
 
-    def _enqueue(self):
-        h = handle(self.device)
-        q, g, mode = self.q, self.g, self.mode
-        check(lib.cmve_pack_rows(h, C.byref(q.desc)), "cmve_pack_rows")
-        check(lib.cmve_pack_rows(h, C.byref(g.desc)), "cmve_pack_rows")
-        dirs = 0
-        for d_bit, a, b, t in ((_lib.DIR_ROW, q, g, self.row), (_lib.DIR_COL, g, q, self.col)):
-            if t is not None:
-                dirs |= d_bit
-                check(lib.cmve_gt_thresholds(h, C.byref(a.desc), C.byref(b.desc), mode, _ptr(t[0]), _ptr(t[1]),
-                                             _ptr(t[2]), _ptr(t[3]), _ptr(t[4])), "cmve_gt_thresholds")
-        r = self.row[2:] if self.row is not None else (None, None, None)
-        c = self.col[2:] if self.col is not None else (None, None, None)
-        rc = self.row_cnt if self.row is not None else None
-        cc = self.col_cnt if self.col is not None else None
-        self.ws.chunks = 1
-        check(lib.cmve_rank_mfma(h, C.byref(q.desc), C.byref(g.desc), mode, dirs, _ptr(r[1]), _ptr(r[2]),
-                                 _ptr(c[1]), _ptr(c[2]), _ptr(rc), _ptr(cc), _ptr(self.ws.cand), self.ws.cap,
-                                 _ptr(self.ws.count)), "cmve_rank_mfma")
-        check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(rc),
-                                  _ptr(cc), _ptr(self.ws.cand), self.ws.cap, _ptr(self.ws.count)), "cmve_rank_fixup")
-        nq, ng = q.n, g.n
-        if self.row is not None:
-            v = self.row_cnt[:nq].to(torch.int64) + 1
-            self.out[:nq].copy_(torch.where(self.row_empty, torch.full_like(v, ng + 1), v))
-        if self.col is not None:
-            v = self.col_cnt[:ng].to(torch.int64) + 1
-            self.out[nq:nq + ng].copy_(torch.where(self.col_empty, torch.full_like(v, nq + 1), v))
-        self.out[nq + ng:].copy_(self.ws.count[:1])
+    def _alloc(self, cap: int):
+        nbytes = C.c_int64()
+        check(lib.cmve_eval_workspace(C.byref(self.q.desc), C.byref(self.g.desc), int(cap), C.byref(nbytes)),
+              "cmve_eval_workspace")
+        self.ws = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)  # zeroed once (ABI contract)
+        self.cap = int(cap)
+
+    @property
+    def ncand(self) -> int:
+        """Undecided pairs of the last evaluation (synchronises)."""
+        return int(self.out[8].item())
+
+    def _bind(self, rs: RowSet, x):
+        """Point the packed set's raw rows at x (a device tensor of the session dtype, rows contiguous),
+        or copy x into the set's own buffer."""
+        if (torch.is_tensor(x) and x.device == self.device and x.dtype == self.dtype and x.dim() == 2
+                and tuple(x.shape) == tuple(rs.raw.shape) and x.stride(1) == 1 and x.stride(0) >= x.shape[1]):
+            src = x
+        else:
+            src_t = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(x))
+            if tuple(src_t.shape) != tuple(rs.raw.shape):
+                raise ValueError(f"RankSession: expected {tuple(rs.raw.shape)}, got {tuple(src_t.shape)}")
+            rs.raw.copy_(src_t, non_blocking=True)
+            src = rs.raw
+        rs.desc.raw = src.data_ptr()
+        rs.desc.raw_ld = src.stride(0)
+        return src
+
+    def enqueue(self, captions, videos, timing_slot: int = -1):
+        """Enqueue one evaluation on the current stream (no synchronisation).  The inputs must stay
+        alive and unmodified until it completes."""
+        self._bound = (self._bind(self.q, captions), self._bind(self.g, videos))
+        r = self.row if self.row is not None else (None, None)
+        c = self.col if self.col is not None else (None, None)
+        check(lib.cmve_eval_ranks(handle(self.device), C.byref(self.q.desc), C.byref(self.g.desc), self.mode,
+                                  _ptr(r[0]), _ptr(r[1]), _ptr(c[0]), _ptr(c[1]), _ptr(self.ws), self.ws.numel(),
+                                  self.cap, _ptr(self.out), int(timing_slot)), "cmve_eval_ranks")
+
+    def timing(self, slot: int):
+        """(pack+thresholds, rank GEMM, fix-up+ranks) milliseconds of the evaluation that used `slot`."""
+        ms = (C.c_float * 3)()
+        check(lib.cmve_eval_timing(handle(self.device), int(slot), ms), "cmve_eval_timing")
+        return list(ms)
 
     def run(self, captions, videos):
-        """Exact 1-based (t2v, v2t) ranks of new caption / video embeddings (numpy or torch)."""
-        for dst, src in ((self.q.raw, captions), (self.g.raw, videos)):
-            src_t = src if torch.is_tensor(src) else torch.from_numpy(np.ascontiguousarray(src))
-            if tuple(src_t.shape) != tuple(dst.shape):
-                raise ValueError(f"RankSession.run: expected {tuple(dst.shape)}, got {tuple(src_t.shape)}")
-            dst.copy_(src_t, non_blocking=True)
-        cur = torch.cuda.current_stream(self.device)
-        self._stream.wait_stream(cur)
-        with torch.cuda.stream(self._stream):
-            if not self.graph:
-                self._enqueue()
-            elif self._graph is None and self._warm < 2:  # eager warm-up on the capture stream
-                self._enqueue()
-                self._warm += 1
-            else:
-                if self._graph is None:
-                    self._graph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._graph, stream=self._stream):
-                        self._enqueue()
-                torch.cuda.synchronize(self.device)  # see the class note
-                self._graph.replay()
+        """Exact 1-based (t2v ranks, v2t ranks) of new caption / video embeddings (numpy or torch)."""
+        for _attempt in range(4):
+            self.enqueue(captions, videos)
             self.host.copy_(self.out, non_blocking=True)
-        cur.wait_stream(self._stream)
-        self._stream.synchronize()
-        nq, ng = self.q.n, self.g.n
-        npairs = int(self.host[nq + ng])
-        if npairs > self.ws.cap:  # undecided pairs overflowed: grow, re-capture, redo
-            if npairs > 2 * (nq * ng + 1024 * self.g.n_pad):
-                raise _lib.CmveError(f"RankSession: impossible undecided-pair count {npairs} (cap {self.ws.cap}, "
-                                     f"device count {self.ws.count[:2].tolist()}, graph {self._graph is not None})")
-            self.ws.grow(npairs)
-            self._graph, self._warm = None, 0
-            return self.run(captions, videos)
+            torch.cuda.current_stream(self.device).synchronize()
+            need = int(self.host[9])
+            if need == 0:
+                break
+            self._alloc(max(need, 2 * self.cap))  # a bucket overflowed: the counts are incomplete
+        else:
+            raise _lib.CmveError("RankSession: undecided-pair list kept overflowing")
         h = self.host.numpy()
-        t2v = h[:nq].copy() if self.row is not None else None
-        v2t = h[nq:nq + ng].copy() if self.col is not None else None
+        nq, ng, o = self.q.n, self.g.n, _lib.EVAL_OUT_HEAD
+        t2v = h[o:o + nq].copy() if self.row is not None else None
+        v2t = h[o + nq:o + nq + ng].copy() if self.col is not None else None
         return t2v, v2t
 
 
@@ -620,8 +604,16 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
     sel = torch.from_numpy(owners).to(a.device)
     expanded = RowSet(a.raw.index_select(0, sel), eps=a.eps, with_lo=a.has_lo, device=a.device, with_f16=a.has_f16)
     r, _, _ = gt_rank_counts(expanded, b, row_gts=items, mode=mode)
+    n_m = b.n
     p = 0
     for i, l in enumerate(lists):
-        out[i] = r[p:p + len(l)]
+        pi = r[p:p + len(l)].copy()
+        # Items ranked individually: an all-NaN GT item gets n_m.  Several items at n_m are all NaN (a
+        # finite item can only be last in a row without NaN), and NaN items share the row's last
+        # positions n_m - n_nan + 1 .. n_m (AP depends only on the set of positions).
+        last = np.flatnonzero(pi == n_m)
+        if last.size > 1:
+            pi[last] = n_m - last.size + 1 + np.arange(last.size)
+        out[i] = pi
         p += len(l)
     return out

@@ -34,33 +34,9 @@ int check_launch(const char* what) {
 // ---------------------------------------------------------------------------
 // K1: pack
 // ---------------------------------------------------------------------------
-// one element of a normalised row -> bf16 hi / bf16 lo / fp16 planes, with the squared residuals
-// of each representation accumulated in fp64 (the bounds are computed from the values STORED,
-// so the f16 conversion need not be correctly rounded from fp64: it goes through fp32, which the
-// hardware converts directly -- gfx950 has no fp64 -> fp16 instruction)
-struct PackAcc {
-  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
-};
-__device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h, uint16_t& l, uint16_t& f,
-                                          PackAcc& acc) {
-  const float xf = (float)xh;
-  if (want_f16) {
-    const _Float16 hf16 = (_Float16)xf;
-    const double r3 = xh - (double)hf16;
-    acc.e3 = fma(r3, r3, acc.e3);
-    f = __builtin_bit_cast(uint16_t, hf16);
-  }
-  h = f2bf(xf);
-  const float hf = bf2f(h);
-  l = f2bf(xf - hf);
-  const double r1 = xh - (double)hf;
-  const double r2 = r1 - (double)bf2f(l);
-  acc.e1 = fma(r1, r1, acc.e1);
-  acc.e2 = fma(r2, r2, acc.e2);
-}
-
 // One wave per row.  VEC: fp32 rows with d % 4 == 0 and 16-B aligned rows -- each lane moves 4
 // consecutive elements (16-B loads, 8-B plane stores); otherwise one element per lane step.
+// (row_sumsq / pack_row_planes, cmve_internal.h: the K14 evaluation kernel packs with the same code)
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ raw, int64_t ld, int64_t n,
                                                         int64_t d, int64_t n_pad, int64_t d_pad, double eps, int flags,
@@ -68,7 +44,6 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
                                                         uint16_t* __restrict__ h16, double* __restrict__ inv_norm,
                                                         float* __restrict__ err_hi, float* __restrict__ err_hilo,
                                                         float* __restrict__ err_h16, float* __restrict__ err_max) {
-  typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_pad) return;
@@ -76,12 +51,7 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
   uint16_t* lrow = lo ? lo + row * d_pad : nullptr;
   uint16_t* frow = h16 ? h16 + row * d_pad : nullptr;
   if (row >= n) {  // padding rows: zero vectors, zero bounds
-    const u16x4 z = {0, 0, 0, 0};
-    for (int64_t k = lane * 4; k < d_pad; k += 256) {  // d_pad % 64 == 0
-      *(u16x4*)(hrow + k) = z;
-      if (lrow) *(u16x4*)(lrow + k) = z;
-      if (frow) *(u16x4*)(frow + k) = z;
-    }
+    pack_pad_row(hrow, lrow, frow, d_pad, lane);
     if (lane == 0) {
       inv_norm[row] = 0.0;
       err_hi[row] = 0.f;
@@ -91,64 +61,15 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const T* __restrict__ ra
     return;
   }
   const T* x = raw + row * ld;
-  double ss = 0.0;
-  if constexpr (VEC) {
-    for (int64_t k = lane * 4; k < d; k += 256) {
-      const float4 v = *(const float4*)(x + k);
-      ss = fma((double)v.x, (double)v.x, ss);
-      ss = fma((double)v.y, (double)v.y, ss);
-      ss = fma((double)v.z, (double)v.z, ss);
-      ss = fma((double)v.w, (double)v.w, ss);
-    }
-  } else {
-    for (int64_t k = lane; k < d; k += 64) {
-      const double v = (double)x[k];
-      ss = fma(v, v, ss);
-    }
-  }
-  ss = wave_sum(ss);
-  const double nrm = sqrt(ss);
   // eps == 0: LINAS l2norm (X / norm, NaN on a zero row); eps > 0: F.normalize
-  const double inv = (flags & CMVE_PACK_RAW) ? 1.0 : (eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm);
-  const bool want_f16 = frow != nullptr;
-  PackAcc acc;
-  if constexpr (VEC) {
-    for (int64_t k = lane * 4; k < d_pad; k += 256) {
-      u16x4 hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0}, fv = {0, 0, 0, 0};
-      if (k < d) {  // d % 4 == 0: all four valid
-        const float4 v = *(const float4*)(x + k);
-        const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          uint16_t h, l, f = 0;
-          pack_elem((double)e[c] * inv, want_f16, h, l, f, acc);
-          hv[c] = h;
-          lv[c] = l;
-          fv[c] = f;
-        }
-      }
-      *(u16x4*)(hrow + k) = hv;
-      if (lrow) *(u16x4*)(lrow + k) = lv;
-      if (frow) *(u16x4*)(frow + k) = fv;
-    }
-  } else {
-    for (int64_t k = lane; k < d_pad; k += 64) {
-      uint16_t h = 0, l = 0, f = 0;
-      if (k < d) pack_elem((double)x[k] * inv, want_f16, h, l, f, acc);
-      hrow[k] = h;
-      if (lrow) lrow[k] = l;
-      if (frow) frow[k] = f;
-    }
-  }
-  const double e1 = wave_sum(acc.e1), e2 = wave_sum(acc.e2), e3 = wave_sum(acc.e3);
+  const double inv = row_inv_norm(row_sumsq<T>(x, d, VEC, lane), eps, flags);
+  float b1, b2, b3;
+  pack_row_planes<T>(x, d, d_pad, VEC, inv, hrow, lrow, frow, lane, b1, b2, b3);
   if (lane == 0) {
     inv_norm[row] = inv;
-    // sqrt rounding + the fp64 error of x*inv itself (~1e-16 per element) -> small slack
-    const float b1 = f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12);
-    const float b2 = f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12);
     err_hi[row] = b1;
     err_hilo[row] = b2;
-    if (err_h16) err_h16[row] = f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12);
+    if (err_h16) err_h16[row] = b3;
   }
 }
 

@@ -16,6 +16,8 @@ struct cmve_handle {
   hipEvent_t ev[CMVE_MAX_CHUNKS + 2] = {};
   hipEvent_t tev[2 * CMVE_MAX_CHUNKS] = {};  // timing: around each chunk's MFMA pass
   int last_chunks = 0;
+  // timing events of cmve_eval_ranks (a ring of CMVE_EVAL_TIMING_SLOTS x 4, created on first use)
+  hipEvent_t eval_ev[CMVE_EVAL_TIMING_SLOTS][4] = {};
   // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -115,17 +117,6 @@ __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB*
   return wave_sum(acc);
 }
 
-// order-preserving uint32 key of an fp32 score (larger score -> larger key); NaN -> 0 (ranks
-// last, as np.argsort puts NaN errors last)
-__device__ __forceinline__ uint32_t topk_key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if (f != f) return 0u;
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float topk_key_inv(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
 // fp64 -> fp32 with directed rounding
 __device__ __forceinline__ float f32_round_up(double x) {
   float f = (float)x;
@@ -138,18 +129,128 @@ __device__ __forceinline__ float f32_round_down(double x) {
   return f;
 }
 
-// Rigorous bound on |score_mfma(i,j) - cos_exact(i,j)| for row errors ea, eb (DESIGN.md s4):
-//   representation:  ea + (1 + ea) * eb          (Cauchy-Schwarz on x_hat - x_tilde)
-//   accumulation:    gamma_n * (1 + ea) * (1 + eb)
-// n counts roundings as if every product and the C operand of each 32-deep
-// v_mfma_f32_16x16x32 were added with its own rounding (33 per 32 products), at
-// u = 2^-23 (2x RNE: covers the truncating alignment the MFMA probe shows -- it drops
-// product bits below ~2^-24 of the largest term, tests/test_gpu_numerics.py).
-__host__ __device__ __forceinline__ double score_error_bound(double ea, double eb, int64_t d_pad, int mode) {
-  const double n = (double)d_pad * (33.0 / 32.0) * (mode == CMVE_SIM_BF16X3 ? 3.0 : 1.0);
-  const double u = 1.0 / 8388608.0;  // 2^-23
-  const double gamma = n * u / (1.0 - n * u);
-  return ea + (1.0 + ea) * eb + gamma * (1.0 + ea) * (1.0 + eb) + 1e-12;
+// ---- K1 row packing (shared by pack_rows_kernel and the K14 evaluation kernel, so a row packs to the
+// same bits on either path) ----
+// sum of squares of one raw row in fp64: VEC (fp32, d % 4 == 0, 16-B aligned) float4 runs per lane
+template <typename T>
+__device__ __forceinline__ double row_sumsq(const T* __restrict__ x, int64_t d, bool vec, int lane) {
+  double ss = 0.0;
+  if constexpr (std::is_same<T, float>::value) {
+    if (vec) {
+      for (int64_t k = (int64_t)lane * 4; k < d; k += 256) {
+        const float4 v = *(const float4*)(x + k);
+        ss = fma((double)v.x, (double)v.x, ss);
+        ss = fma((double)v.y, (double)v.y, ss);
+        ss = fma((double)v.z, (double)v.z, ss);
+        ss = fma((double)v.w, (double)v.w, ss);
+      }
+      return wave_sum(ss);
+    }
+  }
+  for (int64_t k = lane; k < d; k += WAVE) {
+    const double v = (double)x[k];
+    ss = fma(v, v, ss);
+  }
+  return wave_sum(ss);
+}
+// 1/||x||: eps == 0 is LINAS l2norm (no epsilon: a zero row gives inf, hence NaN elements), eps > 0
+// F.normalize; CMVE_PACK_RAW operands are not normalised
+__device__ __forceinline__ double row_inv_norm(double ss, double eps, int flags) {
+  const double nrm = sqrt(ss);
+  return (flags & CMVE_PACK_RAW) ? 1.0 : (eps > 0.0 ? 1.0 / fmax(nrm, eps) : 1.0 / nrm);
+}
+
+// one element of a normalised row -> bf16 hi / bf16 lo / fp16 planes, with the squared residuals
+// of each representation accumulated in fp64 (the bounds are computed from the values STORED,
+// so the f16 conversion need not be correctly rounded from fp64: it goes through fp32, which the
+// hardware converts directly -- gfx950 has no fp64 -> fp16 instruction)
+struct PackAcc {
+  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
+};
+__device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h, uint16_t& l, uint16_t& f,
+                                          PackAcc& acc) {
+  const float xf = (float)xh;
+  if (want_f16) {
+    const _Float16 hf16 = (_Float16)xf;
+    const double r3 = xh - (double)hf16;
+    acc.e3 = fma(r3, r3, acc.e3);
+    f = __builtin_bit_cast(uint16_t, hf16);
+  }
+  h = f2bf(xf);
+  const float hf = bf2f(h);
+  l = f2bf(xf - hf);
+  const double r1 = xh - (double)hf;
+  const double r2 = r1 - (double)bf2f(l);
+  acc.e1 = fma(r1, r1, acc.e1);
+  acc.e2 = fma(r2, r2, acc.e2);
+}
+
+typedef unsigned short cmve_u16x4 __attribute__((ext_vector_type(4)));
+
+// zero planes of a padding row (d_pad % 64 == 0)
+__device__ __forceinline__ void pack_pad_row(uint16_t* hrow, uint16_t* lrow, uint16_t* frow, int64_t d_pad,
+                                             int lane) {
+  const cmve_u16x4 z = {0, 0, 0, 0};
+  for (int64_t k = (int64_t)lane * 4; k < d_pad; k += 256) {
+    *(cmve_u16x4*)(hrow + k) = z;
+    if (lrow) *(cmve_u16x4*)(lrow + k) = z;
+    if (frow) *(cmve_u16x4*)(frow + k) = z;
+  }
+}
+
+// pack one row x * inv into the planes (lrow / frow nullable); b1/b2/b3 = rigorous residual bounds of
+// hi, hi+lo and f16 (wave-uniform)
+template <typename T>
+__device__ __forceinline__ void pack_row_planes(const T* __restrict__ x, int64_t d, int64_t d_pad, bool vec,
+                                                double inv, uint16_t* hrow, uint16_t* lrow, uint16_t* frow,
+                                                int lane, float& b1, float& b2, float& b3) {
+  const bool want_f16 = frow != nullptr;
+  PackAcc acc;
+  bool done = false;
+  if constexpr (std::is_same<T, float>::value) {
+    if (vec) {
+      for (int64_t k = (int64_t)lane * 4; k < d_pad; k += 256) {
+        cmve_u16x4 hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0}, fv = {0, 0, 0, 0};
+        if (k < d) {  // d % 4 == 0: all four valid
+          const float4 v = *(const float4*)(x + k);
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            uint16_t h, l, f = 0;
+            pack_elem((double)e[c] * inv, want_f16, h, l, f, acc);
+            hv[c] = h;
+            lv[c] = l;
+            fv[c] = f;
+          }
+        }
+        *(cmve_u16x4*)(hrow + k) = hv;
+        if (lrow) *(cmve_u16x4*)(lrow + k) = lv;
+        if (frow) *(cmve_u16x4*)(frow + k) = fv;
+      }
+      done = true;
+    }
+  }
+  if (!done)
+    for (int64_t k = lane; k < d_pad; k += WAVE) {
+      uint16_t h = 0, l = 0, f = 0;
+      if (k < d) pack_elem((double)x[k] * inv, want_f16, h, l, f, acc);
+      hrow[k] = h;
+      if (lrow) lrow[k] = l;
+      if (frow) frow[k] = f;
+    }
+  const double e1 = wave_sum(acc.e1), e2 = wave_sum(acc.e2), e3 = wave_sum(acc.e3);
+  // sqrt rounding + the fp64 error of x*inv itself (~1e-16 per element) -> small slack
+  b1 = f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12);
+  b2 = f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12);
+  b3 = f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12);
+}
+
+// 1-based GT rank from a better-than-GT count (LINAS-engine/util/metrics.py:137-147): sgt NaN (empty
+// GT list) -> n_m + 1 (metrics.py:140); sgt +inf (every GT scores NaN) -> n_m (np.argsort puts NaN
+// after every finite score; numpy's order among several NaN is implementation-defined: the GT is
+// taken as the last); else count + 1
+__device__ __forceinline__ int64_t gt_rank_of(int32_t cnt, double sgt, int64_t n_m) {
+  return (sgt != sgt) ? n_m + 1 : (sgt == (double)INFINITY ? n_m : (int64_t)cnt + 1);
 }
 
 // Undecided-pair buffer layout (cand, cap uint64 entries), derived from the gallery set alone:
@@ -169,6 +270,89 @@ inline CandLayout cand_layout(int64_t g_n_pad, int64_t cap) {
   return l;
 }
 constexpr int64_t FIXUP_MAX_BUCKETS_PER_XCD = 4096;  // LDS prefix of the XCD-ordered fix-up
+
+// canonical exact score: cos64(x, y) = dot64(raw_x, raw_y) * (inv_x * inv_y), symmetric in (x, y), so
+// the GT-score, fix-up and top-k re-score kernels score a pair bit-identically
+template <typename TA, typename TB>
+__device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double inva, double invb, int64_t d,
+                                             int lane) {
+  return wave_dot64(xa, xb, d, lane) * (inva * invb);
+}
+
+// XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
+// x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
+// on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
+template <typename TQ, typename TG>
+__device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t ldq,
+                                                    const double* __restrict__ qinv, const TG* __restrict__ graw,
+                                                    int64_t ldg, const double* __restrict__ ginv, int64_t d,
+                                                    const double* __restrict__ row_sgt,
+                                                    const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
+                                                    int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
+                                                    int64_t nb, int64_t cap_b) {
+  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int xcd = blockIdx.x & 7;
+  const int64_t nk = xcd < nb ? (nb - xcd + 7) / 8 : 0;
+  if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
+    const int64_t per = (nk + 63) / 64;
+    const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
+    int64_t sum = 0;
+    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + 8 * k], cap_b);
+    int64_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int64_t run = incl - sum;
+    for (int64_t k = k0; k < k1; ++k) {
+      pre[k] = run;
+      run += min((int64_t)cand[xcd + 8 * k], cap_b);
+    }
+    if (lane == 63) pre[nk] = incl;
+  }
+  __syncthreads();
+  const int64_t total = pre[nk];
+  const int64_t stride = (int64_t)(gridDim.x >> 3) * 4;
+  int64_t k = 0;
+  for (int64_t c = (int64_t)(blockIdx.x >> 3) * 4 + wave; c < total; c += stride) {
+    while (pre[k + 1] <= c) ++k;
+    const uint64_t u = cand[nb + (xcd + 8 * k) * cap_b + (c - pre[k])];
+    const int64_t i = (int64_t)(u & 0x7fffffffull);
+    const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
+    const uint32_t flags = (uint32_t)(u >> 62);
+    const double s = wave_cos64(qraw + i * ldq, graw + j * ldg, qinv[i], ginv[j], d, lane);
+    if (lane == 0) {
+      if ((flags & 1u) && row_sgt && s > row_sgt[i]) atomicAdd(&row_cnt[i], 1);
+      if ((flags & 2u) && col_sgt && s > col_sgt[j]) atomicAdd(&col_cnt[j], 1);
+    }
+  }
+}
+
+// order-preserving uint32 key of an fp32 score (larger score -> larger key); NaN -> 0 (ranks
+// last, as np.argsort puts NaN errors last)
+__device__ __forceinline__ uint32_t topk_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if (f != f) return 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float topk_key_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// Rigorous bound on |score_mfma(i,j) - cos_exact(i,j)| for row errors ea, eb (DESIGN.md s4):
+//   representation:  ea + (1 + ea) * eb          (Cauchy-Schwarz on x_hat - x_tilde)
+//   accumulation:    gamma_n * (1 + ea) * (1 + eb)
+// n counts roundings as if every product and the C operand of each 32-deep
+// v_mfma_f32_16x16x32 were added with its own rounding (33 per 32 products), at
+// u = 2^-23 (2x RNE: covers the truncating alignment the MFMA probe shows -- it drops
+// product bits below ~2^-24 of the largest term, tests/test_gpu_numerics.py).
+__host__ __device__ __forceinline__ double score_error_bound(double ea, double eb, int64_t d_pad, int mode) {
+  const double n = (double)d_pad * (33.0 / 32.0) * (mode == CMVE_SIM_BF16X3 ? 3.0 : 1.0);
+  const double u = 1.0 / 8388608.0;  // 2^-23
+  const double gamma = n * u / (1.0 - n * u);
+  return ea + (1.0 + ea) * eb + gamma * (1.0 + ea) * (1.0 + eb) + 1e-12;
+}
 
 // per-row error plane and err_max slot of a sim mode (err_max = {hi, hilo, h16})
 inline const float* mode_err(const cmve_rows_t* r, int mode) {

@@ -1,0 +1,46 @@
+// K14 evaluation (eval.hip): the argument blocks shared by its kernels and the host entry (sim.hip).
+#pragma once
+#include "cmve_internal.h"
+
+namespace cmve {
+
+// one side of the problem: a packed set and the GT lists of the direction whose queries are its rows
+struct EvalSide {
+  const void* raw;
+  int64_t ld;
+  int64_t n, n_pad;
+  int vec;  // fp32 rows, d % 4 == 0, 16-B aligned: float4 runs (pack_rows_kernel's VEC path)
+  int flags;
+  double eps;
+  uint16_t* hi;
+  uint16_t* lo;
+  uint16_t* h16;
+  double* inv;
+  float* err_hi;
+  float* err_hilo;
+  float* err_h16;
+  float* err_max;
+  const int64_t* off;  // GT lists into the OTHER set; nullptr: this direction is off
+  const int32_t* idx;
+  double* sgt;
+  float* thr_hi;
+  float* thr_lo;
+  int32_t* cnt;
+  int64_t* ranks;      // out: 1-based ranks of this direction
+};
+
+struct EvalCommon {
+  int64_t d, d_pad;
+  int mode;
+  unsigned* done;              // [0]: prep arrivals, [1]: fix arrivals (self-resetting, zero at allocation)
+  unsigned long long* bucket;  // bucket counters at the head of the undecided-pair buffer
+  int64_t nb, cap_b;
+  const uint64_t* cand;
+  int64_t* stats;              // out[0, 16)
+};
+
+// phase 0: pack + GT scores + thresholds, phase 1: fix-up + ranks (phase 2 is the rank GEMM, sim.hip)
+int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
+                hipStream_t s);
+
+}  // namespace cmve

@@ -49,8 +49,11 @@ __global__ __launch_bounds__(256) void gt_thr_kernel(const TA* __restrict__ araw
     }
   }
   if (lane == 0) {
-    if (!any) {  // empty GT list (or NaN GT): never counted, the host maps it to n + 1
-      sgt[row] = NAN;
+    if (!any) {
+      // Never counted.  Empty GT list: sgt = NaN (rank n_m + 1, metrics.py:140).  A non-empty list
+      // whose every GT scores NaN (zero-norm row, no eps in l2norm): sgt = +inf (rank n_m -- np.argsort
+      // puts NaN after every finite score; see cmve_gt_ranks for the rule among several NaN).
+      sgt[row] = off[row + 1] > off[row] ? (double)INFINITY : (double)NAN;
       thr_hi[row] = INFINITY;
       thr_lo[row] = INFINITY;
     } else {
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256) void thr_from_sgt_kernel(const double* __restr
   const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (row >= na_pad) return;
   const double s = row < na ? sgt[row] : NAN;
-  if (s != s) {
+  if (!(s < INFINITY)) {  // NaN (no GT) or +inf (every GT scores NaN): never counted
     thr_hi[row] = INFINITY;
     thr_lo[row] = INFINITY;
     return;
@@ -124,9 +127,7 @@ int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* can
   return check_launch("cand_finalize");
 }
 
-// XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
-// x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
-// on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
+// XCD-ordered re-score of the bucketed undecided pairs (fixup_walk, cmve_internal.h)
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -135,43 +136,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
                                                     int64_t nb, int64_t cap_b) {
-  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int xcd = blockIdx.x & 7;
-  const int64_t nk = xcd < nb ? (nb - xcd + 7) / 8 : 0;
-  if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
-    const int64_t per = (nk + 63) / 64;
-    const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
-    int64_t sum = 0;
-    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + 8 * k], cap_b);
-    int64_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    int64_t run = incl - sum;
-    for (int64_t k = k0; k < k1; ++k) {
-      pre[k] = run;
-      run += min((int64_t)cand[xcd + 8 * k], cap_b);
-    }
-    if (lane == 63) pre[nk] = incl;
-  }
-  __syncthreads();
-  const int64_t total = pre[nk];
-  const int64_t stride = (int64_t)(gridDim.x >> 3) * 4;
-  int64_t k = 0;
-  for (int64_t c = (int64_t)(blockIdx.x >> 3) * 4 + wave; c < total; c += stride) {
-    while (pre[k + 1] <= c) ++k;
-    const uint64_t u = cand[nb + (xcd + 8 * k) * cap_b + (c - pre[k])];
-    const int64_t i = (int64_t)(u & 0x7fffffffull);
-    const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
-    const uint32_t flags = (uint32_t)(u >> 62);
-    const double s = cos64(qraw + i * ldq, graw + j * ldg, qinv[i], ginv[j], d, lane);
-    if (lane == 0) {
-      if ((flags & 1u) && row_sgt && s > row_sgt[i]) atomicAdd(&row_cnt[i], 1);
-      if ((flags & 2u) && col_sgt && s > col_sgt[j]) atomicAdd(&col_cnt[j], 1);
-    }
-  }
+  fixup_walk<TQ, TG>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b);
 }
 
 int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs, const double* row_sgt,
@@ -221,7 +186,9 @@ __global__ __launch_bounds__(256) void rank_rows_kernel(const T* __restrict__ e,
   c = wave_sum_i(c);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) cnt[row] = part[0] + part[1] + part[2] + part[3];
+  // every GT NaN: rank n_m (NaN sorts last; the GT taken as the last of the row's NaN entries)
+  if (threadIdx.x == 0)
+    cnt[row] = (!any && off[row + 1] > off[row]) ? (int32_t)(n_cols - 1) : part[0] + part[1] + part[2] + part[3];
 }
 
 // columns of e ranked (the errors.T view): thread per column, rows split over blockIdx.y
@@ -241,7 +208,10 @@ __global__ __launch_bounds__(256) void rank_cols_kernel(const T* __restrict__ e,
       if (v < thr) thr = v;
     }
   }
-  if (!any) return;
+  if (!any) {  // every GT NaN: rank n_m (counts are zeroed by the caller; one split adds n_rows - 1)
+    if (blockIdx.y == 0 && off[col + 1] > off[col]) atomicAdd(&cnt[col], (int)(n_rows - 1));
+    return;
+  }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
   const int64_t r1 = r0 + rows_per_split < n_rows ? r0 + rows_per_split : n_rows;
   int c = 0;
@@ -267,6 +237,19 @@ __global__ __launch_bounds__(256) void gtpos_rows_kernel(const T* __restrict__ e
   const int64_t k0 = off[row];
   const int m = (int)(off[row + 1] - k0);
   if (m == 0) return;
+  // NaN GT items take the last positions of the row, n_cols - n_nan .. n_cols - 1 (np.argsort puts NaN
+  // after every finite score; the order among several NaN is implementation-defined there, and AP
+  // depends only on the set of positions)
+  __shared__ int s_nan_total, s_nan_run;
+  if (threadIdx.x == 0) {
+    int nn = 0;
+    for (int a = 0; a < m; ++a) {
+      const double v = (double)er[idx[k0 + a]];
+      nn += (v != v);
+    }
+    s_nan_total = nn;
+    s_nan_run = 0;
+  }
   for (int base = 0; base < m; base += MAXG) {  // GT lists longer than MAXG: chunks
     const int mc = min(MAXG, m - base);
     if (threadIdx.x == 0) {
@@ -300,7 +283,7 @@ __global__ __launch_bounds__(256) void gtpos_rows_kernel(const T* __restrict__ e
       int run = 0;
       for (int p = 0; p < mc; ++p) {
         run += hist[p];
-        pos[k0 + base + tk[p]] = (tv[p] != tv[p]) ? (int)n_cols : run;
+        pos[k0 + base + tk[p]] = (tv[p] != tv[p]) ? (int)n_cols - s_nan_total + s_nan_run++ : run;
       }
     }
     __syncthreads();
@@ -323,6 +306,12 @@ __global__ __launch_bounds__(256) void gtpos_cols_kernel(const T* __restrict__ e
   int m_max = m;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m_max = max(m_max, __shfl_xor(m_max, o, 64));
+  // NaN GT items: the last positions, n_rows - n_nan .. n_rows - 1 (as gtpos_rows_kernel)
+  int nan_total = 0, nan_run = 0;
+  for (int a = 0; a < m; ++a) {
+    const double t = (double)e[(int64_t)idx[k0 + a] * ld + col];
+    nan_total += (t != t);
+  }
   for (int a = 0; a < m_max; ++a) {
     int c = 0;
     if (a < m) {
@@ -336,15 +325,75 @@ __global__ __launch_bounds__(256) void gtpos_cols_kernel(const T* __restrict__ e
     __syncthreads();
     if (slice == 0 && a < m) {
       const int c0 = cnt[0][lane];
-      pos[k0 + a] = c0 < 0 ? (int)n_rows : c0 + cnt[1][lane] + cnt[2][lane] + cnt[3][lane];
+      pos[k0 + a] = c0 < 0 ? (int)n_rows - nan_total + nan_run : c0 + cnt[1][lane] + cnt[2][lane] + cnt[3][lane];
     }
+    if (a < m && cnt[0][lane] < 0) ++nan_run;
     __syncthreads();
+  }
+}
+
+// 1-based GT ranks from better-than-GT counts (LINAS-engine/util/metrics.py:137-147 on tie-free rows):
+//   sgt NaN  (empty GT list)        -> n_m + 1   (metrics.py:140 initialises rank = n_m + 1)
+//   sgt +inf (every GT scores NaN)  -> n_m       (np.argsort puts NaN after every finite score; with
+//                                                 several NaN in a row numpy's order among them is
+//                                                 implementation-defined: the GT is taken as the last)
+//   else                            -> cnt + 1
+// recall (optional, one block): #(rank<=1), #(rank<=5), #(rank<=10), sum of ranks (metrics.py:149-157).
+__global__ __launch_bounds__(1024) void gt_ranks_kernel(const int32_t* __restrict__ cnt,
+                                                        const double* __restrict__ sgt, int64_t n, int64_t n_m,
+                                                        int64_t* __restrict__ ranks,
+                                                        unsigned long long* __restrict__ recall) {
+  unsigned long long r1 = 0, r5 = 0, r10 = 0, sum = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = gt_rank_of(cnt[i], sgt[i], n_m);
+    if (ranks) ranks[i] = r;
+    r1 += (r <= 1);
+    r5 += (r <= 5);
+    r10 += (r <= 10);
+    sum += (unsigned long long)r;
+  }
+  if (!recall) return;
+  __shared__ unsigned long long part[16][4];
+  for (int o = 32; o >= 1; o >>= 1) {
+    r1 += __shfl_xor(r1, o, 64);
+    r5 += __shfl_xor(r5, o, 64);
+    r10 += __shfl_xor(r10, o, 64);
+    sum += __shfl_xor(sum, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[w][0] = r1;
+    part[w][1] = r5;
+    part[w][2] = r10;
+    part[w][3] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long t = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k][threadIdx.x];
+    recall[threadIdx.x] = t;
   }
 }
 
 }  // namespace cmve
 
 using namespace cmve;
+
+extern "C" int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_t n, int64_t n_m,
+                             int64_t* ranks, int64_t* recall) {
+  CMVE_REQUIRE(h && cnt && sgt, "cmve_gt_ranks: NULL argument");
+  CMVE_REQUIRE(ranks || recall, "cmve_gt_ranks: no output");
+  CMVE_REQUIRE(n >= 0 && n_m >= 0, "cmve_gt_ranks: bad size");
+  if (n == 0) {
+    if (recall) CMVE_HIP(hipMemsetAsync(recall, 0, 4 * sizeof(int64_t), h->stream));
+    return CMVE_OK;
+  }
+  // the recall sums need one block; without them a grid over the rows
+  const unsigned blocks = recall ? 1u : (unsigned)std::min<int64_t>((n + 1023) / 1024, 4096);
+  hipLaunchKernelGGL(gt_ranks_kernel, dim3(blocks), dim3(1024), 0, h->stream, cnt, sgt, n, n_m, ranks,
+                     (unsigned long long*)recall);
+  return check_launch("gt_ranks_kernel");
+}
 
 extern "C" int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a, const cmve_rows_t* b, int32_t mode,
                                   const int64_t* off, const int32_t* idx, double* sgt, float* thr_hi,
@@ -355,7 +404,7 @@ extern "C" int cmve_gt_thresholds(cmve_handle_t h, const cmve_rows_t* a, const c
   CMVE_REQUIRE(mode == CMVE_SIM_BF16 || mode == CMVE_SIM_BF16X3 || mode == CMVE_SIM_F16,
                "cmve_gt_thresholds: unknown mode");
   CMVE_REQUIRE(off && sgt && thr_hi && thr_lo, "cmve_gt_thresholds: NULL output");
-  CMVE_REQUIRE(a->n == 0 || (a->raw && b->raw && idx), "cmve_gt_thresholds: raw rows / idx missing");
+  CMVE_REQUIRE(a->n == 0 || (a->raw && (b->raw || b->n == 0) && idx), "cmve_gt_thresholds: raw rows / idx missing");
   const float* aerr = mode_err(a, mode);
   CMVE_REQUIRE(aerr, "cmve_gt_thresholds: set has no error plane for this mode");
   dim3 grid((unsigned)((a->n_pad + 3) / 4)), block(256);

@@ -1204,3 +1204,159 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
   if (!resid && !bn_scale && relu <= 1) return dispatch<EPI_BIAS>(a, x, w, mode, h->stream);
   return dispatch<EPI_LINEAR>(a, x, w, mode, h->stream);
 }
+
+// ---- K14: the three-launch evaluation (eval.hip) ----
+#include "eval_abi.h"
+
+namespace {
+struct EvalWs {
+  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, cand, total;
+};
+EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  EvalWs w;
+  size_t o = 0;
+  w.done = o;
+  o = up(o + 16);
+  w.q_sgt = o;
+  o = up(o + 8 * (size_t)nq_pad);
+  w.q_hi = o;
+  o = up(o + 4 * (size_t)nq_pad);
+  w.q_lo = o;
+  o = up(o + 4 * (size_t)nq_pad);
+  w.q_cnt = o;
+  o = up(o + 4 * (size_t)nq_pad);
+  w.g_sgt = o;
+  o = up(o + 8 * (size_t)ng_pad);
+  w.g_hi = o;
+  o = up(o + 4 * (size_t)ng_pad);
+  w.g_lo = o;
+  o = up(o + 4 * (size_t)ng_pad);
+  w.g_cnt = o;
+  o = up(o + 4 * (size_t)ng_pad);
+  w.cand = o;
+  o = up(o + 8 * (size_t)cand_cap);
+  w.total = o;
+  return w;
+}
+}  // namespace
+
+extern "C" int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int64_t* bytes) {
+  CMVE_REQUIRE(q && g && bytes, "cmve_eval_workspace: NULL argument");
+  CMVE_REQUIRE(cand_cap > 0, "cmve_eval_workspace: cand_cap must be > 0");
+  *bytes = (int64_t)eval_ws_layout(q->n_pad, g->n_pad, cand_cap).total;
+  return CMVE_OK;
+}
+
+static cmve::EvalSide eval_side(cmve_rows_t* r, const int64_t* off, const int32_t* idx, char* ws, size_t o_sgt,
+                                size_t o_hi, size_t o_lo, size_t o_cnt, int64_t* ranks) {
+  cmve::EvalSide s{};
+  s.raw = r->raw;
+  s.ld = r->raw_ld;
+  s.n = r->n;
+  s.n_pad = r->n_pad;
+  s.vec = r->raw_dtype == CMVE_F32 && r->d % 4 == 0 && r->raw_ld % 4 == 0 && (((uintptr_t)r->raw & 15) == 0);
+  s.flags = r->flags;
+  s.eps = r->eps;
+  s.hi = r->hi;
+  s.lo = r->lo;
+  s.h16 = r->h16;
+  s.inv = r->inv_norm;
+  s.err_hi = r->err_hi;
+  s.err_hilo = r->err_hilo;
+  s.err_h16 = r->err_h16;
+  s.err_max = r->err_max;
+  s.off = off;
+  s.idx = idx;
+  s.sgt = (double*)(ws + o_sgt);
+  s.thr_hi = (float*)(ws + o_hi);
+  s.thr_lo = (float*)(ws + o_lo);
+  s.cnt = (int32_t*)(ws + o_cnt);
+  s.ranks = ranks;
+  return s;
+}
+
+extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode, const int64_t* row_off,
+                               const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx, void* ws,
+                               int64_t ws_bytes, int64_t cand_cap, int64_t* out, int32_t timing_slot) {
+  CMVE_REQUIRE(h, "cmve_eval_ranks: NULL handle");
+  int st = validate_pair(q, g, mode, "cmve_eval_ranks");
+  if (st) return st;
+  CMVE_REQUIRE(q->n > 0 && g->n > 0, "cmve_eval_ranks: both sets need rows");
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm && q->err_hi && q->err_hilo && g->err_hi &&
+                   g->err_hilo && q->err_max && g->err_max,
+               "cmve_eval_ranks: packed-set arrays missing");
+  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "cmve_eval_ranks: sets packed CMVE_PACK_RAW have no score bound");
+  CMVE_REQUIRE((q->raw_dtype == CMVE_F32 || q->raw_dtype == CMVE_F64) &&
+                   (g->raw_dtype == CMVE_F32 || g->raw_dtype == CMVE_F64),
+               "cmve_eval_ranks: raw rows must be F32 or F64");
+  CMVE_REQUIRE(q->raw_ld >= q->d && g->raw_ld >= g->d, "cmve_eval_ranks: raw_ld < d");
+  CMVE_REQUIRE((q->h16 == nullptr) == (q->err_h16 == nullptr) && (g->h16 == nullptr) == (g->err_h16 == nullptr),
+               "cmve_eval_ranks: h16 and err_h16 go together");
+  CMVE_REQUIRE((row_off != nullptr) == (row_idx != nullptr) && (col_off != nullptr) == (col_idx != nullptr),
+               "cmve_eval_ranks: GT offsets and indices go together");
+  CMVE_REQUIRE(row_off || col_off, "cmve_eval_ranks: no direction requested");
+  CMVE_REQUIRE(ws && out, "cmve_eval_ranks: NULL workspace / output");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_ranks: bad timing slot");
+  const EvalWs w = eval_ws_layout(q->n_pad, g->n_pad, cand_cap);
+  CMVE_REQUIRE(cand_cap > 0 && ws_bytes >= (int64_t)w.total, "cmve_eval_ranks: workspace has %lld bytes, needs %lld",
+               (long long)ws_bytes, (long long)w.total);
+  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  CMVE_REQUIRE(l.cap_b > 0, "cmve_eval_ranks: cand_cap %lld cannot hold the %lld bucket counters", (long long)cand_cap,
+               (long long)l.nb);
+  hipEvent_t* ev = nullptr;
+  if (timing_slot >= 0) {
+    ev = h->eval_ev[timing_slot];
+    for (int k = 0; k < 4; ++k)
+      if (!ev[k]) CMVE_HIP(hipEventCreate(&ev[k]));
+  }
+  char* base = (char*)ws;
+  cmve::EvalSide sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, out + CMVE_EVAL_OUT_HEAD);
+  cmve::EvalSide sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt,
+                                out + CMVE_EVAL_OUT_HEAD + q->n);
+  cmve::EvalCommon c{};
+  c.d = q->d;
+  c.d_pad = q->d_pad;
+  c.mode = mode;
+  c.done = (unsigned*)(base + w.done);
+  uint64_t* cand = (uint64_t*)(base + w.cand);
+  c.bucket = (unsigned long long*)cand;
+  c.nb = l.nb;
+  c.cap_b = l.cap_b;
+  c.cand = cand;
+  c.stats = out;
+  const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
+  hipStream_t s = h->stream;
+  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
+  st = cmve::launch_eval(sq, sg, c, qf, gf, 0, s);
+  if (st) return st;
+  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
+  SimArgs a = make_args(q, g, mode);
+  if (row_off) {
+    a.row_hi = sq.thr_hi;
+    a.row_lo = sq.thr_lo;
+    a.row_cnt = sq.cnt;
+  }
+  if (col_off) {
+    a.col_hi = sg.thr_hi;
+    a.col_lo = sg.thr_lo;
+    a.col_cnt = sg.cnt;
+  }
+  set_cand(a, g, cand, cand_cap, out + 10);  // (the epilogue never writes cand_count)
+  st = dispatch<EPI_RANK>(a, q, g, mode, s);
+  if (st) return st;
+  if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
+  st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
+  if (st) return st;
+  if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3) {
+  CMVE_REQUIRE(h && ms3 && slot >= 0 && slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_timing: bad argument");
+  hipEvent_t* ev = h->eval_ev[slot];
+  CMVE_REQUIRE(ev[0] && ev[3], "cmve_eval_timing: slot %d never recorded", slot);
+  CMVE_HIP(hipEventSynchronize(ev[3]));
+  for (int k = 0; k < 3; ++k) CMVE_HIP(hipEventElapsedTime(&ms3[k], ev[k], ev[k + 1]));
+  return CMVE_OK;
+}

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 6
+#define CMVE_ABI_VERSION 7
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -239,7 +239,8 @@ int cmve_gemm_f32_ex(cmve_handle_t h, int32_t transA, int32_t transB, int64_t M,
 /*
  * K5a -- exact fp64 GT scores and rank thresholds for one direction.
  * For every row a of `a_set` with GT list idx[off[a] .. off[a+1]) into `b_set`:
- *   sgt[a]    = max_k cos64(a, b_k)          (NaN if the list is empty)
+ *   sgt[a]    = max_k cos64(a, b_k) over the GTs that score a number
+ *               (NaN if the list is empty, +inf if every GT scores NaN -- a zero-norm row)
  *   thr_hi[a] = fp32 round-up  (sgt + E_a),  thr_lo[a] = fp32 round-down (sgt - E_a)
  * E_a is the rigorous error bound of the `mode` MFMA score.
  * Rows with no GT or padding get thr = +inf (never counted).  Arrays sized a_set->n_pad.
@@ -307,7 +308,7 @@ int cmve_rank_count_overlap(cmve_handle_t h, const cmve_rows_t* q, const cmve_ro
 int cmve_overlap_mfma_ms(cmve_handle_t h, float* ms, int32_t* launches);
 
 /*
- * Thresholds from GIVEN exact GT scores sgt[a_set->n] (NaN = no GT): the sharded path,
+ * Thresholds from GIVEN exact GT scores sgt[a_set->n] (NaN = no GT, +inf = every GT NaN): the sharded path,
  * where the owner rank of a query's GT computes sgt and all-gathers it with the query.
  * thr_hi/thr_lo as cmve_gt_thresholds, against the error bound of `b_set` (the local shard).
  */
@@ -315,10 +316,66 @@ int cmve_rank_thresholds(cmve_handle_t h, const cmve_rows_t* a_set, const cmve_r
                          const double* sgt, float* thr_hi, float* thr_lo);
 
 /*
+ * 1-based GT ranks from the counts of cmve_rank_count and the GT scores of cmve_gt_thresholds
+ * (LINAS-engine/util/metrics.py:137-147):
+ *   ranks[i] = n_m + 1 if sgt[i] is NaN (empty GT list, metrics.py:140),
+ *              n_m     if sgt[i] is +inf (every GT scores NaN: np.argsort puts NaN after every
+ *                      finite score; numpy's order among several NaN is implementation-defined,
+ *                      the GT is taken as the last),
+ *              cnt[i] + 1 otherwise.
+ * ranks (int64[n]) and/or recall (int64[4]: #rank<=1, #rank<=5, #rank<=10, sum of ranks,
+ * metrics.py:149-157) may be NULL.
+ */
+int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_t n, int64_t n_m,
+                  int64_t* ranks, int64_t* recall);
+
+/*
+ * K14 -- one exact two-direction GT-rank evaluation of a resident problem in THREE launches
+ * (the reference's per-validation chain LINAS-engine/validate.py:61-74 / tester.py:133-139:
+ * evaluation.cal_error (evaluation.py:17-21) then util/metrics.eval_q2m t2v and v2t (metrics.py:124-157)).
+ *   launch 1: pack q and g from their raw rows (as cmve_pack_rows), exact fp64 GT scores of both
+ *             directions (as cmve_gt_thresholds), zeroed counters; its last block derives err_max
+ *             and the rank thresholds;
+ *   launch 2: the fused rank GEMM (as cmve_rank_mfma);
+ *   launch 3: the fp64 fix-up (as cmve_rank_fixup); its last block writes the ranks (as cmve_gt_ranks),
+ *             R@K sums and the pair total.
+ * The numbers equal the separate-launch path bit for bit.  q/g: packed sets (their planes, norms and
+ * bounds are written; raw must point at the current rows).  row_off/row_idx: t2v GT lists of q's rows
+ * into g (NULL: t2v off); col_off/col_idx: v2t GT lists of g's rows into q (NULL: v2t off).
+ * ws: cmve_eval_workspace bytes, ZEROED ONCE when allocated (its arrival counters reset themselves).
+ * out (int64, 16 + q->n + g->n): out[0..4) t2v #rank<=1, #<=5, #<=10, sum of ranks; out[4..8) the same
+ * for v2t; out[8] undecided pairs; out[9] 0, or the cand_cap a retry needs (a bucket overflowed: the
+ * ranks are incomplete); out[16 ..] t2v ranks, then v2t ranks (1-based; cmve_gt_ranks' rules).
+ * timing_slot in [0, CMVE_EVAL_TIMING_SLOTS) records handle events around the three launches
+ * (cmve_eval_timing reads them); -1 records none.
+ */
+#define CMVE_EVAL_TIMING_SLOTS 32
+#define CMVE_EVAL_OUT_HEAD 16
+int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int64_t* bytes);
+int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
+                    const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx,
+                    void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out, int32_t timing_slot);
+/* Durations (ms) of the pack+threshold launch, the rank GEMM and the fix-up+ranks launch of the
+ * cmve_eval_ranks call that used `slot` (waits for its last event). */
+int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3);
+
+/*
+ * C3 -- k-way merge of per-shard exact top-k lists (the gallery sharded over ranks, SURVEY.md 8e;
+ * the merge replaces the single-gallery np.argsort(errors[0])[:topK] of LINAS-engine/inference.py:79).
+ * ids/scores: [n_q, lists * k_in] row-major (the all-gathered shard lists of each query side by side);
+ * each run of k_in is sorted (score desc, id asc) with empty slots (id < 0) at its tail.
+ * out: [n_q, k_out], score desc / global id asc, NaN scores after every number, empty slots id -1 /
+ * score NaN.  1 <= lists <= 64.
+ */
+int cmve_merge_topk(cmve_handle_t h, const int64_t* ids, const double* scores, int64_t n_q, int32_t lists,
+                    int32_t k_in, int32_t k_out, int64_t* out_ids, double* out_scores);
+
+/*
  * Rank from a given score matrix (no GEMM): for each row i of errors[n_q, n_m]
  * (f32 or f64, lower = better, as LINAS errors), with GT lists off/idx:
- *   cnt[i] = #{ j : e_ij < min_{k in GT(i)} e_ik }   (0 if GT(i) is empty: the caller
- *   maps empty lists to rank n_m + 1, as metrics.py:140 initialises it).
+ *   cnt[i] = #{ j : e_ij < min_{k in GT(i)} e_ik }   over the GTs that are not NaN
+ *   (0 if GT(i) is empty: the caller maps empty lists to rank n_m + 1, as metrics.py:140
+ *   initialises it; n_m - 1 if every GT is NaN, i.e. rank n_m as cmve_gt_ranks).
  * transposed != 0 ranks the columns of `errors` instead (errors.T rows).
  * Replaces: LINAS-engine/util/metrics.py:124-147 (eval_q2m's argsort loop).
  */

@@ -88,11 +88,9 @@ def gt_ranks(scores, q2m_gts):
     ranks = np.zeros((n_q,), np.int32)
     for i in range(n_q):
         order = np.argsort(scores[i])
-        pos = np.empty(n_m, np.int64)
-        pos[order] = np.arange(n_m)
         rank = n_m + 1
         for k in q2m_gts[i]:
-            rank = min(rank, int(pos[k]) + 1)
+            rank = min(rank, int(np.where(order == k)[0][0]) + 1)
         ranks[i] = rank
     return ranks
 
@@ -194,10 +192,15 @@ def exact_scores64(q, g):
 
 
 def rank_counts(scores_hi_better, gts):
-    """rank_i = 1 + #{j : s_ij > max_{k in GT(i)} s_ik}  (no-GT rows: n_m + 1).
+    """rank_i = 1 + #{j : s_ij > max_{k in GT(i), s_ik not NaN} s_ik}; no-GT rows: n_m + 1;
+    rows whose every GT scores NaN: n_m.
 
     On tie-free rows this equals ``gt_ranks(-s, gts)`` (the argsort form of
-    ``metrics.py:137-147``); it is the form the GPU path implements.
+    ``metrics.py:137-147``) wherever numpy's order is defined: ``np.argsort`` puts NaN after
+    every finite score, so NaN never beats a GT and a lone NaN GT ranks last (n_m).  With
+    several NaN in a row numpy's order among them is implementation-defined (its SIMD sort
+    does not keep index order); the GT is then taken as the last.  This is the form the GPU
+    path implements.
     """
     s = np.asarray(scores_hi_better)
     n_q, n_m = s.shape
@@ -207,8 +210,24 @@ def rank_counts(scores_hi_better, gts):
         if len(g) == 0:
             out[i] = n_m + 1
             continue
-        thr = s[i, g].max()
-        out[i] = 1 + int(np.count_nonzero(s[i] > thr))
+        sg = s[i, g]
+        sg = sg[~np.isnan(sg)]
+        if sg.size == 0:
+            out[i] = n_m
+            continue
+        out[i] = 1 + int(np.count_nonzero(s[i] > sg.max()))
+    return out
+
+
+def argsort_defined(scores_hi_better, gts):
+    """Rows whose reference rank (np.argsort form) is defined independently of numpy's order
+    among NaN: some GT scores a number, or the row holds at most one NaN."""
+    s = np.asarray(scores_hi_better)
+    out = np.ones(s.shape[0], bool)
+    for i in range(s.shape[0]):
+        g = list(gts[i]) if (not isinstance(gts, dict) or i in gts) else []
+        if g and np.all(np.isnan(s[i, g])) and np.count_nonzero(np.isnan(s[i])) > 1:
+            out[i] = False
     return out
 
 

@@ -52,6 +52,54 @@ def retrieval_case(evaluation, validate, metrics, videos, captions, video_ids, c
                 v2t_gt_lens=np.array([len(l) for l in v2t_gt], np.int32))
 
 
+def _defined(scores, lists):
+    """A row's argsort rank is independent of numpy's (implementation-defined) order among NaN
+    unless every GT is NaN and the row holds more than one NaN."""
+    out = np.ones(scores.shape[0], bool)
+    for i, g in enumerate(lists):
+        if g and np.all(np.isnan(scores[i, g])) and np.count_nonzero(np.isnan(scores[i])) > 1:
+            out[i] = False
+    return out
+
+
+def nan_cases(evaluation, validate, metrics):
+    """Case a (fp32): video 7 is zero (its caption v7#0 ranks a lone NaN GT in every t2v row but the
+    zero caption's); caption v3#1 is zero and shares video 3 with two finite captions (a GT list
+    mixing NaN and finite); videos 30-39 have no caption (empty v2t lists).  Case b (fp64): caption
+    v5#0 is zero and is video 5's only caption (a lone NaN GT in the v2t direction)."""
+    out = {}
+    rng = np.random.default_rng(11)
+    for tag, dtype in (("a", np.float32), ("b", np.float64)):
+        nv, d = 40, 64
+        v = rng.standard_normal((nv, d)).astype(dtype)
+        cid = []
+        for i in range(30):
+            for k in range(3 if i == 3 else (2 if i % 4 == 0 else 1)):
+                cid.append(f"v{i}#{k}")
+        owner = np.array([int(c[1:].split("#")[0]) for c in cid])
+        c = (v[owner] + dtype(1.5) * rng.standard_normal((len(cid), d))).astype(dtype)
+        if tag == "a":
+            v[7] = 0.0
+            c[cid.index("v3#1")] = 0.0
+        else:
+            c[cid.index("v5#0")] = 0.0
+        vid = [f"v{i}" for i in range(nv)]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            errors = evaluation.cal_error(v, c, 'cosine')
+            v2t_gt, t2v_gt = metrics.get_gt(vid, cid)
+            t2v_lists = [t2v_gt.get(i, []) for i in range(len(cid))]
+            t2v_ranks = per_query_ranks(metrics, errors, t2v_lists)
+            v2t_ranks = per_query_ranks(metrics, errors.T, v2t_gt)
+        out[f"{tag}_videos"] = v
+        out[f"{tag}_captions"] = c
+        out[f"{tag}_owner"] = owner.astype(np.int32)
+        out[f"{tag}_t2v_ranks"] = t2v_ranks
+        out[f"{tag}_v2t_ranks"] = v2t_ranks
+        out[f"{tag}_t2v_defined"] = _defined(errors, t2v_lists)
+        out[f"{tag}_v2t_defined"] = _defined(errors.T, v2t_gt)
+    return out
+
+
 def main(ref_root):
     evaluation, validate, metrics = _import_reference(ref_root)
     out = {}
@@ -80,6 +128,10 @@ def main(ref_root):
     g64, q32, pick = synth.gallery_queries()
     top = np.stack([np.argsort(evaluation.cal_error(g64, q32[i:i + 1], 'cosine')[0])[:10] for i in range(q32.shape[0])])
     out["infer"] = dict(top10=top.astype(np.int64), pick=pick.astype(np.int64))
+
+    # (iii) NaN cases (zero-norm rows: LINAS l2norm has no epsilon, evaluation.py:10-14), ranked by the
+    # reference's eval_q2m (np.argsort puts NaN after every finite score)
+    out["nan"] = nan_cases(evaluation, validate, metrics)
 
     for name, d in out.items():
         path = os.path.join(HERE, f"retrieval_{name}.npz")

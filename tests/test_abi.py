@@ -17,7 +17,8 @@ def declared_functions():
 def test_header_declares_the_hot_path():
     names = declared_functions()
     for must in ("cmve_pack_rows", "cmve_sim_store", "cmve_gt_thresholds", "cmve_rank_count",
-                 "cmve_rank_from_matrix", "cmve_gt_positions_from_matrix", "cmve_topk"):
+                 "cmve_rank_from_matrix", "cmve_gt_positions_from_matrix", "cmve_topk", "cmve_gt_ranks",
+                 "cmve_eval_ranks", "cmve_eval_workspace", "cmve_merge_topk"):
         assert must in names
 
 
@@ -30,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 6
+    assert _lib.lib.cmve_abi_version() == 7
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)
@@ -65,3 +66,18 @@ def test_topk_batch_workspace_sizes_the_sample():
     assert nf.value >= 16384 * 10240
     assert _lib.lib.cmve_topk_batch_workspace(C.byref(q), C.byref(g), 33, C.byref(ns), C.byref(nf)) < 0
     assert b"k must be" in _lib.lib.cmve_last_error()
+
+
+def test_eval_workspace_layout_host_only():
+    """cmve_eval_workspace (host-only): grows with the candidate capacity and both padded sets; a
+    capacity too small for the bucket counters is refused by cmve_eval_ranks (checked on the GPU)."""
+    from cmve import _lib
+    q, g = _lib.Rows(), _lib.Rows()
+    q.n, q.n_pad, q.d, q.d_pad = 1000, 1024, 1024, 1024
+    g.n, g.n_pad, g.d, g.d_pad = 1000, 1024, 1024, 1024
+    b1, b2 = C.c_int64(), C.c_int64()
+    assert _lib.lib.cmve_eval_workspace(C.byref(q), C.byref(g), 1 << 16, C.byref(b1)) == 0
+    assert _lib.lib.cmve_eval_workspace(C.byref(q), C.byref(g), 1 << 17, C.byref(b2)) == 0
+    assert b2.value - b1.value == 8 << 16
+    assert b1.value >= (8 << 16) + 2 * 1024 * (8 + 4 + 4 + 4)
+    assert _lib.lib.cmve_eval_workspace(C.byref(q), C.byref(g), 0, C.byref(b1)) < 0

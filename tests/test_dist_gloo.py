@@ -1,9 +1,11 @@
 """world_size-2 gloo rehearsal of the sharded-gallery protocol on CPU.
 
-Each rank scores its contiguous gallery shard with the ORACLE (the GPU kernels are covered
-by the -m gpu tests); everything else is the product coordination code of cmve.dist:
-all-gather of queries, all-reduce(MAX) of per-shard GT scores, all-reduce(SUM) of counts,
-global ranks, and the gathered top-k merge.  Results must equal the unsharded oracle."""
+Each rank scores its contiguous gallery shard with the ORACLE and does the shard-local steps (rank
+from the reduced counts, merge of the gathered runs) in numpy: those are HIP kernels in the product
+(cmve_gt_ranks, cmve_merge_topk) and are covered by the -m gpu tests.  Everything collective is the
+product coordination code of cmve.dist: all-gather of queries, the encoded all-reduce(MAX) of
+per-shard GT scores (NaN GTs included), all-reduce(SUM) of counts with the overflow flag, and the
+gather of the per-shard top-k runs.  Results must equal the unsharded oracle."""
 import os
 import socket
 
@@ -38,7 +40,10 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         gts = [list(rng.choice(n_g, size=int(rng.integers(0, 3)), replace=False)) for _ in range(n_q)]
         used = {int(x) for g in gts for x in g}
         zero = [j for j in range(3, n_g, 7) if j not in used]
-        gal[zero] = 0.0  # zero videos (never a GT): NaN scores, ranked last in index order
+        gal[zero] = 0.0  # zero videos (never a GT): NaN scores, ranked last
+        if n_g > 100:  # a zero GT video (a lone NaN GT: rank n_g) and a list mixing it with a finite GT
+            gal[4] = 0.0
+            gts[0], gts[1] = [4], [4, 50]
         qs = gal[[g[0] if g else 0 for g in gts]] + 0.8 * rng.standard_normal((n_q, d))
         lo, hi = D.shard_bounds(n_g, world, rank)
         # each rank contributes its query slice; all-gather restores the global order
@@ -50,21 +55,36 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
         assert bool(D.any_flag(torch.tensor(rank == 1), world)) and not bool(D.any_flag(torch.tensor(False), world))
         s = R.exact_scores64(q_all.numpy(), gal[lo:hi])             # local shard scores (oracle)
         local = D.local_gt_lists(gts, lo, hi)
-        sgt = torch.tensor([s[i, l].max() if l else np.nan for i, l in enumerate(local)], dtype=torch.float64)
+        def shard_sgt(i, l):  # cmve_gt_thresholds' per-shard encoding: NaN none, +inf all-NaN
+            if not l:
+                return np.nan
+            v = s[i, l]
+            return v[~np.isnan(v)].max() if (~np.isnan(v)).any() else np.inf
+        sgt = torch.tensor([shard_sgt(i, l) for i, l in enumerate(local)], dtype=torch.float64)
         sgt = D.merge_gt_scores(sgt, world)
-        cnt = torch.tensor([int(np.count_nonzero(s[i] > sgt[i].item())) if not np.isnan(sgt[i].item()) else 0
+        cnt = torch.tensor([int(np.count_nonzero(s[i] > sgt[i].item())) if np.isfinite(sgt[i].item()) else 0
                             for i in range(n_q)], dtype=torch.int32)
-        cnt = D.reduce_counts(cnt, world)
-        ranks_t = D.ranks_from(cnt, sgt, n_q, n_g)
-        ranks = ranks_t.numpy()
-        rc = D.recall_counts_device(ranks_t).tolist()
+        flag = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)  # one rank's overflow reaches all
+        both = D.reduce_counts(torch.cat([cnt, flag]), world)
+        cnt, ovf = both[:-1], int(both[-1])
+        assert ovf == 1
+        sg = sgt.numpy()
+        ranks = np.where(np.isnan(sg), n_g + 1, np.where(np.isinf(sg), n_g, cnt.numpy().astype(np.int64) + 1))
+        rc = D.recall_counts_device(torch.from_numpy(ranks)).tolist()
         assert rc == [int((ranks <= 1).sum()), int((ranks <= 5).sum()), int((ranks <= 10).sum()), int(ranks.sum())]
         kk = min(k, hi - lo)
         order = np.argsort(-s, axis=1, kind="stable")[:, :kk]
         idx_g = torch.from_numpy(order + lo)
         sc = torch.from_numpy(np.take_along_axis(s, order, axis=1))
         idx_g, sc = D.pad_topk(idx_g, sc, k)
-        top, _ = D.merge_topk(idx_g, sc, k, world)
+        gi, gs = D.gather_topk(idx_g, sc, world)
+        assert gi.shape == (n_q, world * k)
+        top = np.empty((n_q, k), np.int64)
+        for i in range(n_q):  # merge of the gathered runs (cmve_merge_topk on the GPU)
+            ids, scs = gi[i].numpy(), gs[i].numpy()
+            keep = ids >= 0
+            o = np.lexsort((ids[keep], -scs[keep]))[:k]
+            top[i] = ids[keep][o]
         if rank == 0:
             s_full = R.exact_scores64(qs, gal)
             exp_ranks = R.rank_counts(s_full, gts)
@@ -89,18 +109,3 @@ def test_sharded_protocol_world2(n_g):
         assert p.exitcode == 0
     ranks_ok, top_ok = result_q.get()
     assert ranks_ok and top_ok
-
-
-def test_merge_topk_single_shard_is_identity():
-    """world 1: the shard's own top-k (already score desc, id asc) comes back unchanged; padded
-    empty slots read -1 / NaN."""
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    sys.path.insert(0, os.path.join(os.path.dirname(here), "cross-modal-video-engine_amd"))
-    from cmve import dist as D
-    idx = torch.tensor([[5, 2, 9], [1, 0, 3]])
-    sc = torch.tensor([[0.9, 0.5, -float("inf")], [0.7, 0.7, 0.1]], dtype=torch.float64)
-    idx, sc = D.pad_topk(idx, sc, 4)
-    top, s = D.merge_topk(idx, sc, 4, 1)
-    assert top.tolist() == [[5, 2, 9, -1], [1, 0, 3, -1]]
-    assert np.isnan(s[:, 3]).all() and s[0, 2] == -np.inf

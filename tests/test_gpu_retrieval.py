@@ -354,33 +354,108 @@ def test_unpadded_fast_epilogue_each_direction(torch_cuda, dirs, nq, ng):
         assert np.array_equal(c, R.rank_counts(s.T, col_gts))
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_rank_session_replays_match(golden, torch_cuda, graph):
-    """RankSession (resident buffers, one hipGraph per evaluation): C1 ranks equal the golden ranks
-    on every replay, new embeddings give the ranks gt_rank_counts computes for them, and an
-    undecided-pair overflow grows the list and re-captures without changing the result."""
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_rank_session_replays_match(golden, torch_cuda, dtype):
+    """RankSession (resident buffers, cmve_eval_ranks: three launches per evaluation): C1 ranks equal
+    the golden ranks on every repeat with the inputs read in place, new embeddings give the ranks
+    gt_rank_counts computes for them, the on-device R@K sums match the ranks, and an undecided-pair
+    overflow grows the list without changing the result."""
     import torch
     from cmve import engine
     g = golden("retrieval_c1")
     v, c, vid, cid = _c1()
+    if dtype == "f32":
+        v, c = v.astype(np.float32), c.astype(np.float32)
     v2t_gt, t2v_gt = R.get_gt(vid, cid)
     rows = [t2v_gt[i] for i in range(len(cid))]
-    sess = engine.RankSession(len(cid), len(vid), v.shape[1], row_gts=rows, col_gts=v2t_gt,
-                              dtype=torch.float64 if v.dtype == np.float64 else torch.float32, graph=graph)
-    for _ in range(4):  # warm-up, warm-up, capture + replay, replay
-        t2v, v2t = sess.run(c, v)
-        assert np.array_equal(t2v, g["t2v_ranks"]) and np.array_equal(v2t, g["v2t_ranks"])
+    tdt = torch.float64 if dtype == "f64" else torch.float32
+    sess = engine.RankSession(len(cid), len(vid), v.shape[1], row_gts=rows, col_gts=v2t_gt, dtype=tdt)
+    ct, vt = torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda()
+    for _ in range(4):  # device tensors of the session dtype: read in place
+        t2v, v2t = sess.run(ct, vt)
+        if dtype == "f64":
+            assert np.array_equal(t2v, g["t2v_ranks"]) and np.array_equal(v2t, g["v2t_ranks"])
+        h = sess.host.numpy()
+        assert list(h[0:4]) == [int((t2v <= 1).sum()), int((t2v <= 5).sum()), int((t2v <= 10).sum()), int(t2v.sum())]
+        assert list(h[4:8]) == [int((v2t <= 1).sum()), int((v2t <= 5).sum()), int((v2t <= 10).sum()), int(v2t.sum())]
+    e_t, e_v, ncand = engine.gt_rank_counts(engine.RowSet(c, with_lo=False), engine.RowSet(v, with_lo=False),
+                                            row_gts=rows, col_gts=v2t_gt)
+    assert np.array_equal(t2v, e_t) and np.array_equal(v2t, e_v) and sess.ncand == ncand
     rng = np.random.default_rng(8)
     c2 = (c + 0.5 * rng.standard_normal(c.shape)).astype(c.dtype)
-    t2v2, v2t2 = sess.run(c2, v)
+    t2v2, v2t2 = sess.run(c2, v)  # numpy: copied into the session's buffers
     e_t, e_v, _ = engine.gt_rank_counts(engine.RowSet(c2, with_lo=False), engine.RowSet(v, with_lo=False),
                                         row_gts=rows, col_gts=v2t_gt)
     assert np.array_equal(t2v2, e_t) and np.array_equal(v2t2, e_v)
-    sess.ws = engine.RankWorkspace(sess.device, cap=8)
-    sess._graph, sess._warm = None, 2  # capture straight away with the tiny list
-    t2v3, v2t3 = sess.run(c, v)
-    assert sess.ws.cap > 8
-    assert np.array_equal(t2v3, g["t2v_ranks"]) and np.array_equal(v2t3, g["v2t_ranks"])
+    sess._alloc(600)  # 4 buckets: a tiny list overflows, grows and redoes the evaluation
+    t2v3, v2t3 = sess.run(ct, vt)
+    assert sess.cap > 600
+    assert np.array_equal(t2v3, t2v) and np.array_equal(v2t3, v2t)
+
+
+def _nan_case(g, tag):
+    v, c, own = g[tag + "_videos"], g[tag + "_captions"], g[tag + "_owner"]
+    t2v = [[int(o)] for o in own]
+    v2t = [[i for i in range(c.shape[0]) if own[i] == j] for j in range(v.shape[0])]
+    return v, c, t2v, v2t
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_nan_gt_ranks_every_path(golden, torch_cuda, tag):
+    """Zero-norm rows (no eps: NaN scores) ranked as the reference's eval_q2m does (retrieval_nan.npz,
+    generated by importing LINAS-engine/util/metrics.py): a lone NaN GT ranks last, a list mixing NaN
+    and finite GTs takes the finite one, empty lists give n_m + 1.  Every GPU path agrees with the
+    golden on the rows numpy defines, and with the documented rule (n_m) on the others:
+    gt_rank_counts (3 modes), RankSession, the matrix path (cal_perf on a plain ndarray), the sharded
+    coordination (2 shards merged through cmve.dist's own encoding) and the mAP positions."""
+    import torch
+    from cmve import engine, _lib, dist as D
+    from cmve.linas import metrics as M
+    g = golden("retrieval_nan")
+    v, c, t2v, v2t = _nan_case(g, tag)
+    n_v, n_c = v.shape[0], c.shape[0]
+    exp_t = g[tag + "_t2v_ranks"].astype(np.int64)
+    exp_v = g[tag + "_v2t_ranks"].astype(np.int64)
+    ok_t, ok_v = g[tag + "_t2v_defined"], g[tag + "_v2t_defined"]
+    exp_t[~ok_t] = n_v
+    exp_v[~ok_v] = n_c
+    for mode in (_lib.SIM_F16, _lib.SIM_BF16, _lib.SIM_BF16X3):
+        r, cc, _ = engine.gt_rank_counts(engine.RowSet(c), engine.RowSet(v), row_gts=t2v, col_gts=v2t, mode=mode)
+        assert np.array_equal(r, exp_t), (mode, r, exp_t)
+        assert np.array_equal(cc, exp_v), (mode, cc, exp_v)
+    tdt = torch.float32 if c.dtype == np.float32 else torch.float64
+    sess = engine.RankSession(n_c, n_v, c.shape[1], row_gts=t2v, col_gts=v2t, dtype=tdt)
+    r, cc = sess.run(torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    assert np.array_equal(r, exp_t) and np.array_equal(cc, exp_v)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        errors = np.asarray(R.cal_error(v, c))
+    assert np.array_equal(engine.rank_from_matrix(errors, t2v), exp_t)
+    assert np.array_equal(engine.rank_from_matrix(errors, v2t, transposed=True), exp_v)
+    # two shards of the gallery, coordinated by cmve.dist's own per-shard encoding + MAX + decode
+    q = engine.RowSet(c)
+    cuts = [(0, 17), (17, n_v)]
+    shards = [engine.RowSet(v[lo:hi]) for lo, hi in cuts]
+    sgts, cnts = [], []
+    for (lo, hi), sh in zip(cuts, shards):
+        off, idx = sh_csr = engine.csr(D.local_gt_lists(t2v, lo, hi), q.device)
+        sgt, _, _ = engine.gt_thresholds(q, sh, off, idx, _lib.SIM_F16)
+        sgts.append(D.encode_gt_scores(sgt))
+    sgt = D.decode_gt_scores(torch.stack(sgts).max(dim=0).values)
+    for (lo, hi), sh in zip(cuts, shards):
+        hi_t, lo_t = engine.rank_thresholds(q, sh, sgt, _lib.SIM_F16)
+        ws = engine.RankWorkspace(q.device)
+        cnt, _ = engine.rank_count_launch(q, sh, _lib.SIM_F16, row=(sgt, hi_t, lo_t), ws=ws)
+        assert not ws.overflowed()
+        cnts.append(cnt.clone())
+    ranks = D.ranks_from(sum(cnts), sgt, n_c, n_v).cpu().numpy()
+    assert np.array_equal(ranks, exp_t), (ranks, exp_t)
+    # mAP positions of every GT (v2t lists mix NaN and finite captions in case a)
+    pos = M.gt_positions(errors, v2t, transposed=True)
+    for j, l in enumerate(v2t):
+        if not l or not ok_v[j]:
+            continue
+        order = np.argsort(errors[:, j])
+        assert sorted(pos[j]) == sorted(int(np.where(order == k)[0][0]) + 1 for k in l), j
 
 
 def test_raw_packed_sets_rejected_by_rank_and_topk(torch_cuda):

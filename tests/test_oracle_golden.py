@@ -61,3 +61,35 @@ def test_ap_from_positions_matches_apscorer():
         labels = (rng.random(n) < 0.2).astype(np.int64)
         pos = np.nonzero(labels)[0] + 1
         assert abs(R.ap_score(labels) - R.ap_from_positions(pos)) < 1e-12
+
+
+def nan_case(g, tag):
+    """Inputs and GT lists of retrieval_nan.npz case `tag` (ids v{i} / v{owner}#k, get_gt order)."""
+    v, c, own = g[tag + "_videos"], g[tag + "_captions"], g[tag + "_owner"]
+    t2v = [[int(o)] for o in own]
+    v2t = [[i for i in range(c.shape[0]) if own[i] == j] for j in range(v.shape[0])]
+    return v, c, t2v, v2t
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_nan_gt_ranks_match_reference(golden, tag):
+    """Zero-norm rows (l2norm without eps -> NaN scores): the reference's eval_q2m ranks a lone NaN GT
+    last (n_m) and takes the finite GT of a mixed list.  Where numpy's argsort order is defined (not
+    several NaN in a row whose every GT is NaN), the oracle's count form == its argsort form == the
+    reference; elsewhere the count form gives n_m (the GT taken as the last NaN)."""
+    g = golden("retrieval_nan")
+    v, c, t2v, v2t = nan_case(g, tag)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        s = -R.cal_error(v, c)
+    for scores, lists, key in ((s, t2v, "t2v"), (s.T, v2t, "v2t")):
+        ref = g[f"{tag}_{key}_ranks"]
+        ok = g[f"{tag}_{key}_defined"]
+        assert np.array_equal(ok, R.argsort_defined(scores, lists))
+        counts = R.rank_counts(scores, lists)
+        assert np.array_equal(counts[ok], ref[ok])
+        assert np.array_equal(R.gt_ranks(-scores, lists)[ok], ref[ok])
+        assert np.all(counts[~ok] == scores.shape[1])
+    # the fixture holds each case it was built for: a lone NaN GT ranked last, a mixed list, empty lists
+    n_m = v.shape[0]
+    assert any(np.isnan(s[i, l]).all() and g[f"{tag}_t2v_ranks"][i] == n_m for i, l in enumerate(t2v)) or tag == "b"
+    assert tag == "a" or any(np.isnan(s[l, j]).all() and g["b_v2t_ranks"][j] == c.shape[0] for j, l in enumerate(v2t) if l)
