@@ -198,8 +198,8 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
   CMVE_REQUIRE(r->eps >= 0.0, "cmve_pack_rows: eps < 0");
   CMVE_REQUIRE((r->h16 == nullptr) == (r->err_h16 == nullptr), "cmve_pack_rows: h16 and err_h16 go together");
   dim3 grid((unsigned)((r->n_pad + 3) / 4)), block(256);
-  const bool vec = r->raw_dtype == CMVE_F32 && r->d % 4 == 0 && r->raw_ld % 4 == 0 &&
-                   (r->n == 0 || ((uintptr_t)r->raw & 15) == 0);
+  const bool vec = r->n == 0 || (r->raw_dtype == CMVE_F32 ? rows_vec4((const float*)r->raw, r->d, r->raw_ld)
+                                                           : rows_vec4((const double*)r->raw, r->d, r->raw_ld));
 #define PACK(T, V)                                                                                                   \
   hipLaunchKernelGGL((pack_rows_kernel<T, V>), grid, block, 0, h->stream, (const T*)r->raw, r->raw_ld, r->n, r->d, \
                      r->n_pad, r->d_pad, r->eps, r->flags, r->hi, r->lo, r->h16, r->inv_norm, r->err_hi, r->err_hilo,  \
@@ -208,6 +208,8 @@ int cmve_pack_rows(cmve_handle_t h, cmve_rows_t* r) {
     PACK(float, true);
   else if (r->raw_dtype == CMVE_F32)
     PACK(float, false);
+  else if (r->raw_dtype == CMVE_F64 && vec)
+    PACK(double, true);
   else if (r->raw_dtype == CMVE_F64)
     PACK(double, false);
   else {

@@ -77,41 +77,68 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 
 template <typename T> __device__ __forceinline__ double ld64(const T* p) { return (double)(*p); }
 
-// Exact-ish fp64 dot of two raw rows: lane-strided fma chains then a butterfly.
-// The SAME routine serves the GT scores and the fix-up, so a pair scored in both
-// places gets bit-identical values.
+// four consecutive elements of a raw row as doubles (16-B aligned: one float4 or two double2 loads)
+__device__ __forceinline__ void load4d(const float* p, double (&v)[4]) {
+  const float4 x = *(const float4*)p;
+  v[0] = x.x;
+  v[1] = x.y;
+  v[2] = x.z;
+  v[3] = x.w;
+}
+__device__ __forceinline__ void load4d(const double* p, double (&v)[4]) {
+  const double2 x = *(const double2*)p, y = *(const double2*)(p + 2);
+  v[0] = x.x;
+  v[1] = x.y;
+  v[2] = y.x;
+  v[3] = y.y;
+}
+// rows whose elements 4L + 256m + c a lane may read in 16-B pieces
+template <typename T>
+__host__ __device__ __forceinline__ bool rows_vec4(const T* p, int64_t d, int64_t ld) {
+  return (d & 3) == 0 && ((ld * (int64_t)sizeof(T)) & 15) == 0 && (((uintptr_t)p) & 15) == 0;
+}
+
+// Exact-ish fp64 dot of two raw rows: per-lane fma chains then a butterfly.  The SAME routine
+// serves the GT scores, the fix-up and the top-k re-score, so a pair scored in two places gets
+// bit-identical values.
 //
-// fp32 x fp32 rows with d % 4 == 0 and 16-B aligned starts (the bench / evaluation layout): lane
-// L owns elements 4L + 256m + c, c = 0..3, accumulated in (m, c) order from float4 loads, four
-// 256-element strides per trip so eight 16-B loads are in flight (the fix-up re-scores ~1e6
-// random pairs: latency, not arithmetic, bounds it).  The order is a function of the pair alone
-// and symmetric in (a, b), so every caller still gets the same bits for the same pair.
+// Rows with d % 4 == 0 and 16-B aligned starts (the bench / evaluation layout, fp32 or fp64): lane
+// L owns elements 4L + 256m + c, c = 0..3, accumulated in (m, c) order, four 256-element strides per
+// trip so eight 16-B (fp32) or sixteen 16-B (fp64) loads are in flight (the fix-up re-scores random
+// pairs: latency, not arithmetic, bounds it).  The order is a function of the pair alone (not of
+// the element types) and symmetric in (a, b), so every caller gets the same bits for the same pair.
 template <typename TA, typename TB>
 __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB* __restrict__ b,
                                              int64_t d, int lane) {
   double acc = 0.0;
-  if constexpr (std::is_same<TA, float>::value && std::is_same<TB, float>::value) {
-    if ((d & 3) == 0 && ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0) {
-      auto fma4 = [&](const float4& x, const float4& y) {
-        acc = fma((double)x.x, (double)y.x, acc);
-        acc = fma((double)x.y, (double)y.y, acc);
-        acc = fma((double)x.z, (double)y.z, acc);
-        acc = fma((double)x.w, (double)y.w, acc);
-      };
-      int64_t k = (int64_t)lane * 4;
-      for (; k + 768 < d; k += 1024) {
-        const float4 a0 = *(const float4*)(a + k), a1 = *(const float4*)(a + k + 256);
-        const float4 a2 = *(const float4*)(a + k + 512), a3 = *(const float4*)(a + k + 768);
-        const float4 b0 = *(const float4*)(b + k), b1 = *(const float4*)(b + k + 256);
-        const float4 b2 = *(const float4*)(b + k + 512), b3 = *(const float4*)(b + k + 768);
-        fma4(a0, b0);
-        fma4(a1, b1);
-        fma4(a2, b2);
-        fma4(a3, b3);
-      }
-      for (; k < d; k += 256) fma4(*(const float4*)(a + k), *(const float4*)(b + k));
-      return wave_sum(acc);
+  if ((d & 3) == 0 && ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0) {
+    auto fma4 = [&](const double (&x)[4], const double (&y)[4]) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc = fma(x[c], y[c], acc);
+    };
+    int64_t k = (int64_t)lane * 4;
+    for (; k + 768 < d; k += 1024) {
+      double a0[4], a1[4], a2[4], a3[4], b0[4], b1[4], b2[4], b3[4];
+      load4d(a + k, a0);
+      load4d(a + k + 256, a1);
+      load4d(a + k + 512, a2);
+      load4d(a + k + 768, a3);
+      load4d(b + k, b0);
+      load4d(b + k + 256, b1);
+      load4d(b + k + 512, b2);
+      load4d(b + k + 768, b3);
+      fma4(a0, b0);
+      fma4(a1, b1);
+      fma4(a2, b2);
+      fma4(a3, b3);
     }
+    for (; k < d; k += 256) {
+      double x[4], y[4];
+      load4d(a + k, x);
+      load4d(b + k, y);
+      fma4(x, y);
+    }
+    return wave_sum(acc);
   }
   for (int64_t k = lane; k < d; k += WAVE) acc = fma(ld64(a + k), ld64(b + k), acc);
   return wave_sum(acc);
@@ -135,17 +162,14 @@ __device__ __forceinline__ float f32_round_down(double x) {
 template <typename T>
 __device__ __forceinline__ double row_sumsq(const T* __restrict__ x, int64_t d, bool vec, int lane) {
   double ss = 0.0;
-  if constexpr (std::is_same<T, float>::value) {
-    if (vec) {
-      for (int64_t k = (int64_t)lane * 4; k < d; k += 256) {
-        const float4 v = *(const float4*)(x + k);
-        ss = fma((double)v.x, (double)v.x, ss);
-        ss = fma((double)v.y, (double)v.y, ss);
-        ss = fma((double)v.z, (double)v.z, ss);
-        ss = fma((double)v.w, (double)v.w, ss);
-      }
-      return wave_sum(ss);
+  if (vec) {  // rows_vec4: elements 4L + 256m + c (fp32 or fp64 alike)
+    for (int64_t k = (int64_t)lane * 4; k < d; k += 256) {
+      double v[4];
+      load4d(x + k, v);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ss = fma(v[c], v[c], ss);
     }
+    return wave_sum(ss);
   }
   for (int64_t k = lane; k < d; k += WAVE) {
     const double v = (double)x[k];
@@ -207,28 +231,26 @@ __device__ __forceinline__ void pack_row_planes(const T* __restrict__ x, int64_t
   const bool want_f16 = frow != nullptr;
   PackAcc acc;
   bool done = false;
-  if constexpr (std::is_same<T, float>::value) {
-    if (vec) {
-      for (int64_t k = (int64_t)lane * 4; k < d_pad; k += 256) {
-        cmve_u16x4 hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0}, fv = {0, 0, 0, 0};
-        if (k < d) {  // d % 4 == 0: all four valid
-          const float4 v = *(const float4*)(x + k);
-          const float e[4] = {v.x, v.y, v.z, v.w};
+  if (vec) {  // rows_vec4: 16-B loads, four elements per lane step, 8-B plane stores
+    for (int64_t k = (int64_t)lane * 4; k < d_pad; k += 256) {
+      cmve_u16x4 hv = {0, 0, 0, 0}, lv = {0, 0, 0, 0}, fv = {0, 0, 0, 0};
+      if (k < d) {  // d % 4 == 0: all four valid
+        double e[4];
+        load4d(x + k, e);
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            uint16_t h, l, f = 0;
-            pack_elem((double)e[c] * inv, want_f16, h, l, f, acc);
-            hv[c] = h;
-            lv[c] = l;
-            fv[c] = f;
-          }
+        for (int c = 0; c < 4; ++c) {
+          uint16_t h, l, f = 0;
+          pack_elem(e[c] * inv, want_f16, h, l, f, acc);
+          hv[c] = h;
+          lv[c] = l;
+          fv[c] = f;
         }
-        *(cmve_u16x4*)(hrow + k) = hv;
-        if (lrow) *(cmve_u16x4*)(lrow + k) = lv;
-        if (frow) *(cmve_u16x4*)(frow + k) = fv;
       }
-      done = true;
+      *(cmve_u16x4*)(hrow + k) = hv;
+      if (lrow) *(cmve_u16x4*)(lrow + k) = lv;
+      if (frow) *(cmve_u16x4*)(frow + k) = fv;
     }
+    done = true;
   }
   if (!done)
     for (int64_t k = lane; k < d_pad; k += WAVE) {
@@ -282,7 +304,9 @@ __device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double 
 // XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
 // x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
 // on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
-template <typename TQ, typename TG>
+// PREFETCH: load the pair's GT scores before its dot product (latency-bound small evaluations; in the
+// bandwidth-bound bench-size fix-up that was 3% slower)
+template <typename TQ, typename TG, bool PREFETCH = false>
 __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
                                                     int64_t ldg, const double* __restrict__ ginv, int64_t d,
@@ -313,18 +337,24 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
   }
   __syncthreads();
   const int64_t total = pre[nk];
-  const int64_t stride = (int64_t)(gridDim.x >> 3) * 4;
+  const int nw = (int)(blockDim.x >> 6);  // waves per block
+  const int64_t stride = (int64_t)(gridDim.x >> 3) * nw;
   int64_t k = 0;
-  for (int64_t c = (int64_t)(blockIdx.x >> 3) * 4 + wave; c < total; c += stride) {
+  for (int64_t c = (int64_t)(blockIdx.x >> 3) * nw + wave; c < total; c += stride) {
     while (pre[k + 1] <= c) ++k;
     const uint64_t u = cand[nb + (xcd + 8 * k) * cap_b + (c - pre[k])];
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     const uint32_t flags = (uint32_t)(u >> 62);
+    double rs = 0.0, cs = 0.0;
+    if (PREFETCH) {
+      rs = ((flags & 1u) && row_sgt) ? row_sgt[i] : 0.0;
+      cs = ((flags & 2u) && col_sgt) ? col_sgt[j] : 0.0;
+    }
     const double s = wave_cos64(qraw + i * ldq, graw + j * ldg, qinv[i], ginv[j], d, lane);
     if (lane == 0) {
-      if ((flags & 1u) && row_sgt && s > row_sgt[i]) atomicAdd(&row_cnt[i], 1);
-      if ((flags & 2u) && col_sgt && s > col_sgt[j]) atomicAdd(&col_cnt[j], 1);
+      if ((flags & 1u) && row_sgt && s > (PREFETCH ? rs : row_sgt[i])) atomicAdd(&row_cnt[i], 1);
+      if ((flags & 2u) && col_sgt && s > (PREFETCH ? cs : col_sgt[j])) atomicAdd(&col_cnt[j], 1);
     }
   }
 }

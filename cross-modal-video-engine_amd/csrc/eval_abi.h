@@ -4,6 +4,8 @@
 
 namespace cmve {
 
+constexpr int EVAL_ARRIVAL_WORDS = 9 * 64;  // top + 8 shard counters, 256 B apart (eval.hip)
+
 // one side of the problem: a packed set and the GT lists of the direction whose queries are its rows
 struct EvalSide {
   const void* raw;
@@ -32,11 +34,13 @@ struct EvalSide {
 struct EvalCommon {
   int64_t d, d_pad;
   int mode;
-  unsigned* done;              // [0]: prep arrivals, [1]: fix arrivals (self-resetting, zero at allocation)
+  unsigned* done;              // arrival counters: prep at [0, EVAL_ARRIVAL_WORDS), fix-up after them
+                               // (self-resetting, zero at allocation)
   unsigned long long* bucket;  // bucket counters at the head of the undecided-pair buffer
   int64_t nb, cap_b;
   const uint64_t* cand;
   int64_t* stats;              // out[0, 16)
+  int dbg;                     // kernel studies only (CMVE_EVAL_DBG): skip parts, results garbage
 };
 
 // phase 0: pack + GT scores + thresholds, phase 1: fix-up + ranks (phase 2 is the rank GEMM, sim.hip)

@@ -1054,11 +1054,11 @@ extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve
                                const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count) {
   CMVE_REQUIRE(h && q && g, "cmve_rank_fixup: NULL argument");
   CMVE_REQUIRE(q->d == g->d, "cmve_rank_fixup: dimension mismatch");
-  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup: raw rows / norms missing");
   if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_sgt && row_cnt, "cmve_rank_fixup: row arrays missing");
   if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_sgt && col_cnt, "cmve_rank_fixup: col arrays missing");
   CMVE_REQUIRE(cand && cand_count, "cmve_rank_fixup: candidate buffer missing");
-  if (q->n == 0 || g->n == 0) return CMVE_OK;
+  if (q->n == 0 || g->n == 0) return CMVE_OK;  // nothing to re-score (an empty gallery shard)
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup: raw rows / norms missing");
   return launch_fixup(h->stream, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, cand_count);
 }
 
@@ -1122,12 +1122,12 @@ extern "C" int cmve_rank_count_overlap(cmve_handle_t h, const cmve_rows_t* q, co
   int st = rank_args(q, g, mode, dirs, row_hi, row_lo, col_hi, col_lo, row_cnt, col_cnt, cand, cand_cap, cand_count,
                      a, "cmve_rank_count_overlap");
   if (st) return st;
-  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_count_overlap: raw rows / norms missing");
   hipStream_t s0 = h->stream;
   CMVE_HIP(hipMemsetAsync(cand_count, 0, sizeof(int64_t) * chunks, s0));
   if (dirs & CMVE_DIR_ROW) CMVE_HIP(hipMemsetAsync(row_cnt, 0, sizeof(int32_t) * q->n_pad, s0));
   if (dirs & CMVE_DIR_COL) CMVE_HIP(hipMemsetAsync(col_cnt, 0, sizeof(int32_t) * g->n_pad, s0));
   if (q->n == 0 || g->n == 0) return CMVE_OK;
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_count_overlap: raw rows / norms missing");
   st = ensure_aux(h);
   if (st) return st;
   // chunk rows: a multiple of CMVE_ROW_ALIGN covering g->n_pad in `chunks` pieces
@@ -1217,7 +1217,7 @@ EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
   EvalWs w;
   size_t o = 0;
   w.done = o;
-  o = up(o + 16);
+  o = up(o + 2 * sizeof(unsigned) * cmve::EVAL_ARRIVAL_WORDS);
   w.q_sgt = o;
   o = up(o + 8 * (size_t)nq_pad);
   w.q_hi = o;
@@ -1255,7 +1255,8 @@ static cmve::EvalSide eval_side(cmve_rows_t* r, const int64_t* off, const int32_
   s.ld = r->raw_ld;
   s.n = r->n;
   s.n_pad = r->n_pad;
-  s.vec = r->raw_dtype == CMVE_F32 && r->d % 4 == 0 && r->raw_ld % 4 == 0 && (((uintptr_t)r->raw & 15) == 0);
+  s.vec = r->raw_dtype == CMVE_F32 ? rows_vec4((const float*)r->raw, r->d, r->raw_ld)
+                                    : rows_vec4((const double*)r->raw, r->d, r->raw_ld);
   s.flags = r->flags;
   s.eps = r->eps;
   s.hi = r->hi;
@@ -1325,6 +1326,11 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   c.cap_b = l.cap_b;
   c.cand = cand;
   c.stats = out;
+  static const int dbg = [] {
+    const char* e = getenv("CMVE_EVAL_DBG");  // kernel studies only
+    return e ? atoi(e) : 0;
+  }();
+  c.dbg = dbg;
   const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
   hipStream_t s = h->stream;
   if (ev) CMVE_HIP(hipEventRecord(ev[0], s));

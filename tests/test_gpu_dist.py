@@ -22,9 +22,9 @@ def _problem(n_g=1500, n_q=400, d=96, seed=21):
     rng = np.random.default_rng(seed)
     gal = rng.standard_normal((n_g, d)).astype(np.float32)
     gts = [[int(x) for x in rng.choice(n_g, size=int(rng.integers(0, 3)), replace=False)] for _ in range(n_q)]
-    gts[0], gts[1], gts[2] = [7], [7, 900], []      # a lone NaN GT, a NaN + finite list, no GT
+    gts[0], gts[1], gts[2] = [7], [7, n_g - 100], []  # a lone NaN GT, a NaN + finite list, no GT
     qs = (gal[[g[0] if g else 0 for g in gts]] + 1.2 * rng.standard_normal((n_q, d))).astype(np.float32)
-    gal[[7, 40, 1203]] = 0.0                          # zero videos: NaN columns
+    gal[[7, 40, n_g - 297]] = 0.0                     # zero videos: NaN columns
     return gal, qs, gts
 
 
