@@ -352,6 +352,7 @@ __device__ __forceinline__ void prep_tail(const EvalSide& q, const EvalSide& g, 
 
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(EVAL_NT) void eval_prep_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  EVAL_STAMP(c, 0, 0);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * EVAL_NW + (threadIdx.x >> 6);
   for (int64_t t = (int64_t)blockIdx.x * EVAL_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * EVAL_NT)
@@ -362,10 +363,13 @@ __global__ __launch_bounds__(EVAL_NT) void eval_prep_kernel(EvalSide q, EvalSide
     else if (row < q.n_pad + g.n_pad)
       prep_row<TG, TQ>(g, q, c, row - q.n_pad, lane);
   }
+  EVAL_STAMP(c, 0, 1);
   if (c.dbg & 2) return;
   if (!last_block_arrival(c.done)) return;
+  EVAL_STAMP(c, 0, 2);
   if (c.dbg & 4) return;
   prep_tail(q, g, c);
+  EVAL_STAMP(c, 0, 3);
 }
 
 // The last block of the fix-up launch: pair total / overflow size (cand_finalize_kernel's), the ranks
@@ -426,13 +430,17 @@ __device__ __forceinline__ void fix_tail(const EvalSide& q, const EvalSide& g, c
 
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(EVAL_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  EVAL_STAMP(c, 2, 0);
   if (!(c.dbg & 8))
     fixup_walk<TQ, TG, true>((const TQ*)q.raw, q.ld, q.inv, (const TG*)g.raw, g.ld, g.inv, c.d, q.off ? q.sgt : nullptr,
                        g.off ? g.sgt : nullptr, q.cnt, g.cnt, c.cand, c.nb, c.cap_b);
+  EVAL_STAMP(c, 2, 1);
   if (c.dbg & 16) return;
   if (!last_block_arrival(c.done + EVAL_ARRIVAL_WORDS)) return;
+  EVAL_STAMP(c, 2, 2);
   if (c.dbg & 32) return;
   fix_tail(q, g, c);
+  EVAL_STAMP(c, 2, 3);
 }
 
 template <typename TQ, typename TG>

@@ -41,9 +41,14 @@ struct EvalCommon {
   const uint64_t* cand;
   int64_t* stats;              // out[0, 16)
   int dbg;                     // kernel studies only (CMVE_EVAL_DBG): skip parts, results garbage
+  unsigned long long* stamps;  // kernel studies only (CMVE_EVAL_DBG & 128): [kernel][block][4] s_memrealtime
 };
 
 // phase 0: pack + GT scores + thresholds, phase 1: fix-up + ranks (phase 2 is the rank GEMM, sim.hip)
+// stamp k of block b in kernel kern (0 prep, 1 rank GEMM, 2 fix-up) when stamps are on
+#define EVAL_STAMP(cp, kern, k)                                                                                  \
+  if ((cp).stamps && threadIdx.x == 0)                                                                           \
+  (cp).stamps[((size_t)(kern) * 1024 + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memrealtime()
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s);
 

@@ -1241,6 +1241,16 @@ EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
 }
 }  // namespace
 
+static unsigned long long* g_eval_stamps = nullptr;
+// kernel studies only (not in cmve.h): copy the last CMVE_EVAL_DBG & 128 stamps to the host
+extern "C" int cmve_eval_debug_stamps(void* host, int64_t bytes) {
+  CMVE_REQUIRE(g_eval_stamps && host, "cmve_eval_debug_stamps: no stamps (CMVE_EVAL_DBG & 128)");
+  CMVE_HIP(hipDeviceSynchronize());
+  CMVE_HIP(hipMemcpy(host, g_eval_stamps, std::min<int64_t>(bytes, sizeof(unsigned long long) * 3 * 1024 * 4),
+                     hipMemcpyDeviceToHost));
+  return CMVE_OK;
+}
+
 extern "C" int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int64_t* bytes) {
   CMVE_REQUIRE(q && g && bytes, "cmve_eval_workspace: NULL argument");
   CMVE_REQUIRE(cand_cap > 0, "cmve_eval_workspace: cand_cap must be > 0");
@@ -1331,6 +1341,10 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     return e ? atoi(e) : 0;
   }();
   c.dbg = dbg;
+  static unsigned long long* stamp_buf = nullptr;
+  if ((dbg & 128) && !stamp_buf) CMVE_HIP(hipMalloc(&stamp_buf, sizeof(unsigned long long) * 3 * 1024 * 4));
+  c.stamps = (dbg & 128) ? stamp_buf : nullptr;
+  g_eval_stamps = c.stamps;
   const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
   hipStream_t s = h->stream;
   if (ev) CMVE_HIP(hipEventRecord(ev[0], s));

@@ -501,3 +501,33 @@ def test_bench_shape_ranks_against_independent_fp64(torch_cuda):
         exp[b:b + 128] = 1 + (s > sg).sum(dim=1).cpu().numpy()
     got = t2v[rows.cpu().numpy()]
     assert (got != exp).sum() <= 1, np.nonzero(got != exp)
+
+
+@pytest.mark.parametrize("nq,ng,d", [(3, 129, 100), (130, 257, 64), (1000, 1000, 1024), (257, 300, 1536),
+                                     (2000, 600, 512), (64, 5000, 128)])
+def test_rank_session_shapes_against_oracle(torch_cuda, nq, ng, d):
+    """cmve_eval_ranks on ragged shapes (G128 and G256 rank GEMMs), empty GT lists and multi-GT lists,
+    fp32 and fp64 rows: ranks == the oracle's exact counts, R@K sums == the ranks'."""
+    import torch
+    from cmve import engine
+    rng = np.random.default_rng(nq + 7 * ng + d)
+    gal = rng.standard_normal((ng, d))
+    qs = gal[rng.integers(0, ng, nq)] + 0.7 * rng.standard_normal((nq, d))
+    row_gts = [[] if i % 7 == 6 else [int(x) for x in rng.choice(ng, size=1 + i % 2, replace=False)]
+               for i in range(nq)]
+    col_gts = [[] if j % 5 == 4 else [int(x) for x in rng.choice(nq, size=min(nq, 1 + j % 3), replace=False)]
+               for j in range(ng)]
+    s = R.exact_scores64(qs, gal)
+    exp_r, exp_c = R.rank_counts(s, row_gts), R.rank_counts(s.T, col_gts)
+    for dt in (torch.float64, torch.float32):
+        sess = engine.RankSession(nq, ng, d, row_gts=row_gts, col_gts=col_gts, dtype=dt)
+        q_t = torch.from_numpy(qs).to("cuda", dt)
+        g_t = torch.from_numpy(gal).to("cuda", dt)
+        r, c = sess.run(q_t, g_t)
+        if dt == torch.float32:  # the oracle on the fp32-rounded rows
+            s32 = R.exact_scores64(q_t.double().cpu().numpy(), g_t.double().cpu().numpy())
+            exp_r, exp_c = R.rank_counts(s32, row_gts), R.rank_counts(s32.T, col_gts)
+        assert np.array_equal(r, exp_r) and np.array_equal(c, exp_c), dt
+        h = sess.host.numpy()
+        assert list(h[0:4]) == [int((r <= 1).sum()), int((r <= 5).sum()), int((r <= 10).sum()), int(r.sum())]
+        assert list(h[4:8]) == [int((c <= 1).sum()), int((c <= 5).sum()), int((c <= 10).sum()), int(c.sum())]
