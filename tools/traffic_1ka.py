@@ -1,0 +1,71 @@
+"""Reduce the rocprofv3 passes of tools/profile_1ka.sh to per-launch figures of the three K14
+evaluation launches (pack + GT scores, rank GEMM, fix-up + ranks) of the 1k-A headline.
+
+HBM bytes per dispatch = 2 * FETCH_SIZE(KiB) * 1024 + WRITE_SIZE(KiB) * 1024 (gfx950 FETCH_SIZE
+half-count on wide reads, MI355X_MICROARCH.md).  Writes profiles/<tag>_1ka_traffic.json (read by
+bench.py) and copies the kernel-stats summary to profiles/<tag>_1ka_kernel_stats.csv.
+    python tools/traffic_1ka.py <outdir> <tag>"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def role(name):
+    if "eval_prep_kernel" in name:
+        return "pack_gt_thresholds"
+    if "eval_fix_kernel" in name:
+        return "fixup_ranks"
+    if "sim_kernel<2, 1" in name:
+        return "rank_gemm"
+    return None
+
+
+def main(outdir, tag):
+    prof = os.path.join(outdir, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(outdir, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_1ka_kernel_stats.csv"))
+    per = defaultdict(lambda: defaultdict(list))
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        for r in rows(os.path.join(outdir, sub, "**", "*counter_collection.csv")):
+            k = role(r.get("Kernel_Name", ""))
+            if k and r.get("Counter_Name") == counter:
+                per[k][counter].append(float(r["Counter_Value"]))
+    dur = defaultdict(list)
+    for r in rows(os.path.join(outdir, "trace", "**", "*kernel_trace.csv")):
+        k = role(r.get("Kernel_Name", ""))
+        if k:
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    kernels = {}
+    for k in ("pack_gt_thresholds", "rank_gemm", "fixup_ranks"):
+        f, w = per[k]["FETCH_SIZE"], per[k]["WRITE_SIZE"]
+        e = {"launches_traced": len(dur[k]),
+             "trace_avg_ms": (sum(dur[k]) / len(dur[k])) if dur[k] else None,
+             "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
+             "write_kib_per_launch": (sum(w) / len(w)) if w else None}
+        if f and w:
+            e["hbm_bytes_per_launch"] = 2 * e["fetch_kib_per_launch"] * 1024 + e["write_kib_per_launch"] * 1024
+        kernels[k] = e
+    out = {"tag": tag, "workload": "MSR-VTT-1kA exact evaluation, 1000 x 1000 x 1024, float64 inputs",
+           "kernels": kernels,
+           "hbm_bytes_per_launch": kernels["rank_gemm"].get("hbm_bytes_per_launch"),
+           "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"}
+    json.dump(out, open(os.path.join(prof, f"{tag}_1ka_traffic.json"), "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
