@@ -160,6 +160,11 @@ class VideoBatchLoader:
     def __len__(self):
         return (len(self.video_ids) + self.batch_size - 1) // self.batch_size
 
+    @property
+    def dataset(self):
+        """The videos in loader order (``len(loader.dataset)`` as evaluation.encode_vid reads it)."""
+        return self.video_ids
+
     def batch(self, b: int):
         vids = self.video_ids[b * self.batch_size:(b + 1) * self.batch_size]
         idxs = tuple(range(b * self.batch_size, b * self.batch_size + len(vids)))
@@ -189,7 +194,15 @@ class VideoBatchLoader:
 
 
 def load_video_cache(path: str):
-    """inference.py:57-60 ``video_data.pt`` cache {'video_embs', 'video_ids'}, loaded with
-    ``weights_only=True`` (no code executed); a cache the safe loader refuses raises."""
-    d = torch.load(path, weights_only=True, map_location="cpu")
+    """inference.py:57-60 ``video_data.pt`` cache {'video_embs', 'video_ids'} (the float64 ndarray
+    encode_vid returns and the id list), loaded with ``weights_only=True`` and numpy's array
+    reconstruction admitted (no code executed); a cache the safe loader refuses raises."""
+    from .checkpoint import _safe_globals
+    with torch.serialization.safe_globals(_safe_globals()):
+        d = torch.load(path, weights_only=True, map_location="cpu")
     return d["video_embs"], list(d["video_ids"])
+
+
+def save_video_cache(path: str, video_embs, video_ids):
+    """inference.py:67: torch.save({'video_embs', 'video_ids'}) as the reference writes it."""
+    torch.save({"video_embs": video_embs, "video_ids": list(video_ids)}, path)

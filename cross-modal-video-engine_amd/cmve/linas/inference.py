@@ -10,16 +10,21 @@ queries (the GEMM beyond), a histogram bound on the k-th score, and an exact fp6
 of the error band: same ids, same order (score desc; ties by index) as the reference's
 argsort on tie-free scores.
 
-CLI (same flags as inference.py:37-44, plus the inputs the frozen encoder would make):
-  python -m cmve.linas.inference --input "a man ..." --topK 10 --gpu 0 \
-      --gallery video_data.npz --query-emb cap.npy
-``--gallery`` is an .npz with ``video_embs`` [N, D] and ``video_ids`` (the content of the
-reference's ``video_data.pt`` cache, inference.py:57-67); ``--query-emb`` is the caption
-embedding that ``model.embed_txt_distill(process_cap(input))`` produces (inference.py:76-77).
-With ``--checkpoint`` (the reference's model_best.pth.tar, loaded weights-only) and the two
-vocabularies, ``--input`` is encoded exactly as inference.py:69-77 does (cmve.linas.text.process_cap
--> cmve.linas.checkpoint.QueryEncoder); the reference's own checkpoint
-``student_support_set_8/model_best.pth.tar`` is not shipped (LINAS-engine/readme.md:17).
+CLI (same flags and flow as inference.py:37-82; run from the directory that holds the
+reference's ``student_support_set_8/`` and ``dataset/``):
+  python -m cmve.linas.inference --input "a man ..." --topK 10 --gpu 0
+  1. checkpoint ``student_support_set_8/model_best.pth.tar`` -> get_model(opt.model)(opt),
+     load_state_dict(checkpoint['model'], 'test'), val_start (weights-only load, cmve.linas.checkpoint)
+  2. gallery: ``video_data.pt`` if it exists (weights-only), else BigFile features of
+     dataset/<test collection>/FeatureData/<visual_feature> + video2frames.txt -> encode_vid(
+     model.embed_vis_distill, ...) on the GPU, written back to ``video_data.pt``
+  3. vocabularies dataset/<train collection>/TextData/vocabulary/{bow,rnn}/<vocab>.pkl (restricted
+     unpickler) -> process_cap(--input) -> embed_txt_distill
+  4. exact top-K of the cosine errors on HBM (GalleryScorer), printed as the id list
+``--gpu`` is exported as HIP_VISIBLE_DEVICES before the GPU is touched (the reference's
+CUDA_VISIBLE_DEVICES, inference.py:47); its default is '0' rather than the reference's '5', which
+would hide every GPU of a box with fewer than six.  ``--query-emb`` (a .npy caption embedding)
+and ``--gallery`` (an .npz with video_embs / video_ids) bypass steps 3 and 1-2 respectively.
 """
 from __future__ import annotations
 
@@ -81,35 +86,72 @@ def parse_args(argv=None):
     p.add_argument('--input', default='a man and a woman is talking.', type=str, help='input sentence')
     p.add_argument('--topK', default=10, type=int, help='return top-k videos')
     p.add_argument('--gpu', default='0', type=str, help='gpu device')
-    p.add_argument('--gallery', default='video_data.npz', type=str,
-                   help='npz with video_embs [N,D] and video_ids (the video_data.pt cache content)')
+    p.add_argument('--checkpoint', default='student_support_set_8/model_best.pth.tar', type=str,
+                   help='LINAS model_best.pth.tar (inference.py:49), loaded weights-only')
+    p.add_argument('--rootpath', default='dataset/', type=str, help='dataset root (inference.py:55)')
+    p.add_argument('--video-cache', default='video_data.pt', type=str,
+                   help='gallery cache {video_embs, video_ids} (inference.py:57-67)')
+    p.add_argument('--gallery', default=None, type=str,
+                   help='.npz with video_embs [N,D] and video_ids instead of the cache / BigFile')
     p.add_argument('--query-emb', default=None, type=str,
-                   help='.npy caption embedding [1,D] (output of the frozen text encoder for --input)')
-    p.add_argument('--checkpoint', default=None, type=str,
-                   help='LINAS model_best.pth.tar: encode --input with its text encoder + mapping '
-                        '(loaded weights-only, cmve.linas.checkpoint)')
-    p.add_argument('--rnn-vocab', default=None, type=str, help='rnn vocabulary (.json or the reference .pkl)')
-    p.add_argument('--bow-vocab', default=None, type=str, help='bow vocabulary (.json or the reference .pkl)')
+                   help='.npy caption embedding [1,D] instead of encoding --input')
+    p.add_argument('--rnn-vocab', default=None, type=str, help='rnn vocabulary (default: the checkpoint opt path)')
+    p.add_argument('--bow-vocab', default=None, type=str, help='bow vocabulary (default: the checkpoint opt path)')
     return p.parse_args(argv)
+
+
+def _gallery(opt, model, options):
+    """inference.py:57-67: the video_data.pt cache, else encode_vid over the BigFile features."""
+    from . import bigfile as B
+    if opt.gallery is not None:
+        data = np.load(opt.gallery, allow_pickle=False)
+        return data['video_embs'], [str(v) for v in data['video_ids']]
+    if os.path.exists(opt.video_cache):
+        return B.load_video_cache(opt.video_cache)
+    if model is None:
+        sys.exit("cmve inference: no gallery (give --gallery, a %s cache, or the checkpoint)" % opt.video_cache)
+    from .evaluation import encode_vid
+    feat_dir = os.path.join(opt.rootpath, options.collections_pathname['test'], 'FeatureData', options.visual_feature)
+    visual_feats = B.BigFile(feat_dir)
+    video2frames = B.read_dict(os.path.join(feat_dir, 'video2frames.txt'))
+    loader = B.VideoBatchLoader(visual_feats, video2frames, video_ids=list(video2frames.keys()),
+                                batch_size=options.batch_size, device=model.device)
+    video_embs, video_ids = encode_vid(model.embed_vis_distill, loader)
+    B.save_video_cache(opt.video_cache, video_embs, video_ids)
+    return video_embs, video_ids
 
 
 def main(argv=None):
     opt = parse_args(argv)
-    os.environ.setdefault("HIP_VISIBLE_DEVICES", opt.gpu)
-    if opt.query_emb is None and not (opt.checkpoint and opt.rnn_vocab and opt.bow_vocab):
-        sys.exit("cmve inference: give --query-emb, or --checkpoint with --rnn-vocab and --bow-vocab "
-                 "(inference.py:49-77: checkpoint + vocabularies -> process_cap -> embed_txt_distill)")
-    data = np.load(opt.gallery, allow_pickle=False)
-    scorer = GalleryScorer(data['video_embs'], [str(v) for v in data['video_ids']])
+    os.environ["HIP_VISIBLE_DEVICES"] = opt.gpu
+    model = options = None
+    if opt.query_emb is None or (opt.gallery is None and not os.path.exists(opt.video_cache)):
+        from .checkpoint import load_checkpoint, get_model
+        checkpoint = load_checkpoint(opt.checkpoint)
+        options = checkpoint['opt']
+        model = get_model(options.model)(options)
+        model.load_state_dict(checkpoint['model'], 'test')
+        model.Eiters = checkpoint['Eiters']
+        model.val_start()
+    video_embs, video_ids = _gallery(opt, model, options)
     if opt.query_emb is not None:
         cap_emb = np.load(opt.query_emb, allow_pickle=False).astype(np.float32)
     else:
-        from .checkpoint import QueryEncoder
         from . import text as T
-        enc = QueryEncoder.from_checkpoint(opt.checkpoint)
-        vocab, bow_vocab = T.load_vocab(opt.rnn_vocab), T.load_vocab(opt.bow_vocab)
-        cap_emb = enc(T.process_cap(opt.input, vocab, T.get_text_encoder('bow')(bow_vocab))).cpu().numpy()
-    print(scorer.topk_ids(cap_emb, opt.topK))
+        voc = os.path.join(opt.rootpath, options.collections_pathname['train'], 'TextData', 'vocabulary')
+        bow_vocab = T.load_vocab(opt.bow_vocab or os.path.join(voc, 'bow', options.vocab + '.pkl'))
+        vocab = T.load_vocab(opt.rnn_vocab or os.path.join(voc, 'rnn', options.vocab + '.pkl'))
+        bow2vec = T.get_text_encoder('bow')(bow_vocab)
+        cap_emb = model.embed_txt_distill(T.process_cap(opt.input, vocab, bow2vec)).cpu().numpy()
+    measure = getattr(options, 'measure', 'cosine') if options is not None else 'cosine'
+    if measure == 'cosine':
+        results = GalleryScorer(video_embs, [str(v) for v in video_ids]).topk_ids(cap_emb, opt.topK)
+    else:  # inference.py:78-80 with a cdist / jaccard measure: the all-pairs kernel, then argsort
+        from .evaluation import cal_error
+        errors = np.asarray(cal_error(video_embs, cap_emb, measure))
+        results = [video_ids[i] for i in np.argsort(errors[0])[:opt.topK]]
+    print(results)
+    return results
 
 
 if __name__ == '__main__':

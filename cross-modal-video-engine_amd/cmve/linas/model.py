@@ -4,6 +4,8 @@
   MFC(fc_layers, dropout, ...)            model.py:51-116  (eval forward: fused GEMM epilogue, K3)
   Latent_mapping(mapping_layers, ...)     model.py:362-381 (MFC + BN + l2norm)
   temporal pools                          model.py:152-166 (gru mean / masked max / max_pool1d)
+  Video_multilevel_encoding(opt)          model.py:119-188 (eval forward: frozen biGRU / Conv2d in
+                                          PyTorch-ROCm, every pool on K2)
 Modules keep the reference's parameter names, so reference checkpoints load with
 ``load_state_dict`` (slot layout model.py:387-404).  Inference (eval) runs on the HIP kernels;
 training mode (batch-statistics BN, dropout, autograd backward) runs on the K11 functions of
@@ -184,3 +186,41 @@ def video_level_features(gru_init_out, videos_mask, lengths, videos_origin, conv
     if concate == "full":
         return torch.cat((gru_out, con_out, videos_origin), 1)
     return torch.cat((gru_out, con_out), 1)
+
+
+class Video_multilevel_encoding(nn.Module):
+    """model.py:119-188, eval forward.  Same submodule names (``rnn``, ``convs1``) and state-dict
+    keys as the reference, so its checkpoint slots load unchanged; the biGRU and the Conv2d bank
+    are the frozen backbones (PyTorch-ROCm), the temporal pools run on K2 (video_level_features).
+
+    As in the reference the GRU runs over the zero-padded batch (no packing, model.py:150), and
+    the conv max-pool spans the batch's padded width, so an embedding depends on the batch it is
+    encoded in (the collate of encode_vid fixes that batch)."""
+
+    def __init__(self, opt):
+        super().__init__()
+        self.rnn_output_size = opt.visual_rnn_size * 2
+        self.dropout = nn.Dropout(p=opt.dropout)
+        self.concate = opt.concate
+        self.gru_pool = opt.gru_pool
+        self.tag_vocab_size = getattr(opt, "tag_vocab_size", None)
+        self.loss_fun = getattr(opt, "loss_fun", "mrl")
+        self.rnn = nn.GRU(opt.visual_feat_dim, opt.visual_rnn_size, batch_first=True, bidirectional=True)
+        self.convs1 = nn.ModuleList([
+            nn.Conv2d(1, opt.visual_kernel_num, (w, self.rnn_output_size), padding=(w - 1, 0))
+            for w in opt.visual_kernel_sizes])
+
+    def forward(self, videos):
+        if self.training:
+            raise NotImplementedError("cmve Video_multilevel_encoding is the frozen gallery-side backbone: "
+                                      "call .eval()")
+        vids, videos_origin, lengths, videos_mask = videos
+        with torch.no_grad():
+            gru_init_out, _ = self.rnn(vids)
+            return video_level_features(gru_init_out, videos_mask, lengths, videos_origin, self.convs1,
+                                        gru_pool=self.gru_pool, concate=self.concate)
+
+    def load_state_dict(self, state_dict, strict=True):
+        """model.py:178-188: keep only this module's keys (a full model's state dict loads)."""
+        own = self.state_dict()
+        return super().load_state_dict({k: v for k, v in state_dict.items() if k in own}, strict=strict)

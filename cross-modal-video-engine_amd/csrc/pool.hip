@@ -10,6 +10,9 @@
 //                                                  MCT/mmaction/models/recognizers/recognizer2d.py:76-83 (TSN)
 //       MAX_MASKED_ZERO  max_t x[t] * mask[t]      LINAS-engine/model.py:157-158 (masked steps contribute 0)
 //       MAX_ALL          max over all T            LINAS-engine/model.py:163-166 (max_pool1d over padded length)
+//   cmve_adaptive_avg_pool2d -- F.adaptive_avg_pool2d of the reference video's middle tokens
+//       (MultiFusion/src/inference.py:58-59: [1, T, 18*18, C] -> [1, T, 16, D]); windows
+//       [floor(i*H/OH), ceil((i+1)*H/OH)) x [floor(j*W/OW), ceil((j+1)*W/OW)) as ATen defines them.
 #include "cmve_internal.h"
 
 namespace cmve {
@@ -110,9 +113,48 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ x, 
   }
 }
 
+// block = (output row i, plane p): the window's input rows are summed per column into LDS (one
+// coalesced pass over the rows, each input row read by at most two blocks), then each thread sums
+// the column window of its output columns and divides by the window area.
+__global__ __launch_bounds__(256) void adaptive_avg_kernel(const float* __restrict__ x, int64_t H, int64_t W,
+                                                           int64_t sp, int64_t sh, int64_t OH, int64_t OW,
+                                                           float* __restrict__ out) {
+  extern __shared__ float colsum[];
+  const int64_t i = blockIdx.x, p = blockIdx.y;
+  const int64_t hs = (i * H) / OH, he = ((i + 1) * H + OH - 1) / OH;
+  const float* src = x + p * sp;
+  for (int64_t c = threadIdx.x; c < W; c += 256) {
+    float s = 0.f;
+    for (int64_t r = hs; r < he; ++r) s += src[r * sh + c];
+    colsum[c] = s;
+  }
+  __syncthreads();
+  const float rows = (float)(he - hs);
+  for (int64_t j = threadIdx.x; j < OW; j += 256) {
+    const int64_t ws = (j * W) / OW, we = ((j + 1) * W + OW - 1) / OW;
+    float s = 0.f;
+    for (int64_t c = ws; c < we; ++c) s += colsum[c];
+    out[(p * OH + i) * OW + j] = s / (rows * (float)(we - ws));
+  }
+}
+
 }  // namespace cmve
 
 using namespace cmve;
+
+extern "C" int cmve_adaptive_avg_pool2d(cmve_handle_t h, const float* x, int64_t P, int64_t H, int64_t W,
+                                        int64_t sp, int64_t sh, int64_t OH, int64_t OW, float* out) {
+  CMVE_REQUIRE(h && x && out, "cmve_adaptive_avg_pool2d: NULL argument");
+  CMVE_REQUIRE(P >= 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && sh >= W && sp >= (H - 1) * sh + W,
+               "cmve_adaptive_avg_pool2d: bad shape");
+  CMVE_REQUIRE(W * (int64_t)sizeof(float) <= 64 * 1024, "cmve_adaptive_avg_pool2d: W=%lld exceeds the LDS row",
+               (long long)W);
+  CMVE_REQUIRE(OH <= 65535 * 1024 && P <= 65535, "cmve_adaptive_avg_pool2d: grid too large");
+  if (P == 0) return CMVE_OK;
+  hipLaunchKernelGGL(adaptive_avg_kernel, dim3((unsigned)OH, (unsigned)P), dim3(256), W * sizeof(float), h->stream,
+                     x, H, W, sp, sh, OH, OW, out);
+  return check_launch("adaptive_avg_kernel");
+}
 
 extern "C" int cmve_collate_frames(cmve_handle_t h, const float* frames, int64_t ldf, const int64_t* offsets,
                                    int64_t B, int64_t F, int32_t max_len, int32_t t_max, float* videos,

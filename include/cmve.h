@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 7
+#define CMVE_ABI_VERSION 8
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -161,6 +161,14 @@ int cmve_collate_frames(cmve_handle_t h, const float* frames, int64_t ldf, const
 int cmve_temporal_pool(cmve_handle_t h, const float* x, int64_t stride_b, int64_t stride_t,
                        int64_t B, int64_t T, int64_t F, const int32_t* lengths, int32_t mode,
                        float* out, int64_t ldo);
+
+/* K2 -- F.adaptive_avg_pool2d of the reference video's middle tokens before the single-query
+ * combine (MultiFusion/src/inference.py:58-59: [1, T, 18*18, C] -> [1, T, 16, D]).
+ * x: P planes of [H, W] fp32 (plane stride sp, row stride sh, columns contiguous);
+ * out: [P, OH, OW] contiguous; ATen's windows [floor(i*H/OH), ceil((i+1)*H/OH)) per axis.
+ * W <= 16384. */
+int cmve_adaptive_avg_pool2d(cmve_handle_t h, const float* x, int64_t P, int64_t H, int64_t W,
+                             int64_t sp, int64_t sh, int64_t OH, int64_t OW, float* out);
 
 /*
  * K8/K9 -- non-GEMM pieces of MultiFusion Combiner.combine_features (MultiFusion/src/combiner.py:19-43,146-180):

@@ -147,3 +147,16 @@ BIGFILE_REQUESTS = [
     ["vid003_2", "vid000_1", "nope", "vid003_2", "orphan_4"],   # duplicate + unknown name
     ["vid001_%d" % k for k in range(80, 0, -3)],              # reverse order
 ]
+
+
+def multifusion_query(seed=31, frames=8, channels=1280, n_gallery=200, d=640):
+    """One composed query of MultiFusion/src/inference.py:124-136: reference high features [f, d],
+    middle tokens [f, 18*18, channels], the CLIP text feature [1, d], the target videos' high
+    features [n_gallery, f, d] and their paths (fp32)."""
+    rng = np.random.default_rng(seed)
+    high = rng.standard_normal((frames, d), dtype=np.float32)
+    mid = rng.standard_normal((frames, 18 * 18, channels), dtype=np.float32)
+    text = rng.standard_normal((1, d), dtype=np.float32)
+    gallery = rng.standard_normal((n_gallery, frames, d), dtype=np.float32)
+    names = [f"../dataset/videos/V{i:04d}.mp4" for i in range(n_gallery)]
+    return high, mid, text, gallery, names
