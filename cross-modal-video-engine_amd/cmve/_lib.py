@@ -30,6 +30,7 @@ EVAL_OUT_HEAD = 16
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD = 0, 1, 2, 3, 4
+PAIR_MSE, PAIR_SMOOTH_L1, PAIR_KL = 0, 1, 2
 
 
 class Rows(C.Structure):
@@ -61,6 +62,8 @@ SIGNATURES = {
     "cmve_linear": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64]),
     "cmve_collate_frames": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
     "cmve_temporal_pool": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64]),
+    "cmve_pair_loss_fwd": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, C.c_float, _vp]),
+    "cmve_pair_loss_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, C.c_float, _vp, _vp, _vp]),
     "cmve_adaptive_avg_pool2d": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "cmve_layernorm": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _i64]),
     "cmve_mha_1q": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64]),
@@ -122,7 +125,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -11,6 +11,11 @@
 //   K7  InfoNCE      MultiFusion/src/combiner_train.py:318,367-372 (CE(100 * P.T^T, arange): row half)
 //       and its transpose (MCT/mmaction/models/backbones/clip.py:383-386): the col half.
 //       loss_row = mean_i (lse_j(t S_ij) - t S_ii), loss_col = mean_j (lse_i(t S_ij) - t S_jj).
+//   K15 element-pair losses of the distillation step (LINAS-engine/model.py:554-580,845-895):
+//       MSE (x-y)^2 (nn.MSELoss), SmoothL1 beta 1 (nn.SmoothL1Loss: 0.5 d^2 if |d| < 1 else |d| - 0.5),
+//       KLDiv (nn.KLDivLoss, log_target False: xlogy(y, y) - y x -- NaN for y < 0, as torch), each
+//       optionally weighted per element (the 'diag' / 'adapt' similarity variants) and scaled
+//       (sum / mean / * batchsize); backward d/dx and d/dy with torch's formulas.
 // Reductions are deterministic (fixed order, single block for the final sum).
 #include "cmve_internal.h"
 
@@ -328,9 +333,87 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(const float* __
   }
 }
 
+// ---------------- K15: element-pair losses ----------------
+__device__ __forceinline__ float pair_f(int kind, float x, float y) {
+  if (kind == 0) {
+    const float d = x - y;
+    return d * d;
+  }
+  if (kind == 1) {
+    const float d = x - y, a = fabsf(d);
+    return a < 1.f ? 0.5f * d * d : a - 0.5f;
+  }
+  // xlogy(y, y) - y * x: 0 * log 0 = 0, log of a negative target is NaN
+  const float xl = (y == 0.f) ? 0.f : y * logf(y);
+  return xl - y * x;
+}
+
+__global__ __launch_bounds__(1024) void pair_loss_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                         const float* __restrict__ w, int64_t n, int kind, float scale,
+                                                         float* __restrict__ loss) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    float f = pair_f(kind, x[i], y[i]);
+    if (w) f *= w[i];
+    s += (double)f;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += red[k];
+    loss[0] = (float)(t * (double)scale);
+  }
+}
+
+__global__ __launch_bounds__(256) void pair_grad_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                        const float* __restrict__ w, int64_t n, int kind, float scale,
+                                                        const float* __restrict__ g, float* __restrict__ dx,
+                                                        float* __restrict__ dy) {
+  const float gs = g[0] * scale;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float xv = x[i], yv = y[i];
+    float gx, gy;
+    if (kind == 0) {
+      gx = 2.f * (xv - yv);
+      gy = -gx;
+    } else if (kind == 1) {
+      const float d = xv - yv;
+      gx = d < -1.f ? -1.f : (d > 1.f ? 1.f : d);
+      gy = -gx;
+    } else {
+      gx = -yv;
+      gy = yv > 0.f ? logf(yv) + 1.f - xv : NAN;
+    }
+    const float c = w ? gs * w[i] : gs;
+    if (dx) dx[i] = c * gx;
+    if (dy) dy[i] = c * gy;
+  }
+}
+
 }  // namespace cmve
 
 using namespace cmve;
+
+extern "C" int cmve_pair_loss_fwd(cmve_handle_t h, const float* x, const float* y, const float* w, int64_t n,
+                                  int32_t kind, float scale, float* loss) {
+  CMVE_REQUIRE(h && loss && (n == 0 || (x && y)), "cmve_pair_loss_fwd: NULL argument");
+  CMVE_REQUIRE(n >= 0 && kind >= 0 && kind <= 2, "cmve_pair_loss_fwd: bad size / kind %d", kind);
+  hipLaunchKernelGGL(pair_loss_kernel, dim3(1), dim3(1024), 0, h->stream, x, y, w, n, kind, scale, loss);
+  return check_launch("pair_loss_fwd");
+}
+
+extern "C" int cmve_pair_loss_bwd(cmve_handle_t h, const float* x, const float* y, const float* w, int64_t n,
+                                  int32_t kind, float scale, const float* g, float* dx, float* dy) {
+  CMVE_REQUIRE(h && g && (n == 0 || (x && y)), "cmve_pair_loss_bwd: NULL argument");
+  CMVE_REQUIRE(n >= 0 && kind >= 0 && kind <= 2, "cmve_pair_loss_bwd: bad size / kind %d", kind);
+  if (n == 0 || (!dx && !dy)) return CMVE_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(pair_grad_kernel, dim3(blocks), dim3(256), 0, h->stream, x, y, w, n, kind, scale, g, dx, dy);
+  return check_launch("pair_loss_bwd");
+}
 
 extern "C" int cmve_triplet_fwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float margin,
                                 int32_t max_violation, int32_t dir, int32_t mean_style, float* loss,

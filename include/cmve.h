@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 8
+#define CMVE_ABI_VERSION 9
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -233,6 +233,19 @@ int cmve_infonce_fwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, flo
                      float* loss3, double* row_lse, double* col_lse, float* row_loss, float* col_loss);
 int cmve_infonce_bwd(cmve_handle_t h, const float* S, int64_t ld, int32_t B, float scale, int32_t dir,
                      const float* g, const double* row_lse, const double* col_lse, float* dS, int64_t ldd);
+
+/*
+ * K15 -- element-pair losses of the distillation step (LINAS-engine/model.py:554-580 criteria,
+ * :845-895 forward_loss_distill_similarity / forward_loss_distill):
+ *   kind 0 MSE (x-y)^2, 1 SmoothL1 (beta 1), 2 KLDiv (input x, target y, log_target False:
+ *   xlogy(y, y) - y*x, NaN for y < 0 as torch).  loss (device f32[1]) = scale * sum_i w_i f(x_i, y_i)
+ *   (w nullable = 1; fp64 accumulation, one block: deterministic).  bwd: dx_i = g*scale*w_i*df/dx,
+ *   dy_i = g*scale*w_i*df/dy (either output nullable), g = device f32[1] upstream gradient.
+ */
+int cmve_pair_loss_fwd(cmve_handle_t h, const float* x, const float* y, const float* w, int64_t n,
+                       int32_t kind, float scale, float* loss);
+int cmve_pair_loss_bwd(cmve_handle_t h, const float* x, const float* y, const float* w, int64_t n,
+                       int32_t kind, float scale, const float* g, float* dx, float* dy);
 
 /* fp32 GEMM for the loss gradient products and the training heads: C = alpha * op(A) . op(B) + beta * C
  * (op = transpose when trans* != 0; row-major) on v_mfma_f32_16x16x4_f32 -- each output is exactly a
