@@ -29,7 +29,7 @@ EVAL_TIMING_SLOTS = 32
 EVAL_OUT_HEAD = 16
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
-PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD = 0, 1, 2, 3, 4
+PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD, PW_DOT = 0, 1, 2, 3, 4, 5
 PAIR_MSE, PAIR_SMOOTH_L1, PAIR_KL = 0, 1, 2
 
 

@@ -585,11 +585,36 @@ def topk(q: RowSet, g: RowSet, k: int, mode: int = _lib.SIM_F16, scores_ws: Opti
                             scores_ws.numel(), _ptr(idx), _ptr(sc), _ptr(ovf)), "cmve_topk")
         if int(ovf.item()) == 0:
             break
-    else:
-        raise _lib.CmveError("topk: the error band kept more than 4096 columns for some query")
+    else:  # a query's error band held > TOPK_CAP columns (near-duplicate gallery rows at the k-th score)
+        idx, sc = _topk_dense_exact(q, g, k)
+        if not to_host:
+            return idx, sc
+        return idx.to(torch.int64).cpu().numpy(), sc.cpu().numpy()
     if not to_host:
         return idx[:q.n], sc[:q.n]
     return idx[:q.n].to(torch.int64).cpu().numpy(), sc[:q.n].cpu().numpy()
+
+
+def _topk_dense_exact(q: RowSet, g: RowSet, k: int, gallery_chunk: int = 1 << 16):
+    """Exact top-k by dense fp64 scoring (the fallback of topk when an error band overflows): the
+    normalised rows in fp64, gallery chunks scored by the K10 DOT kernel (a k-ordered fp64 fma chain
+    per pair, so exact duplicates score identically -- a library dgemm rounds by tile position), each
+    chunk stable-sorted (score desc, index asc; NaN last as np.argsort of the errors) and merged with
+    the running top-k."""
+    qn = q.normalized(torch.float64)
+    best_s = torch.full((q.n, 0), float("-inf"), dtype=torch.float64, device=q.device)
+    best_i = torch.zeros((q.n, 0), dtype=torch.int64, device=q.device)
+    gn_all = g.normalized(torch.float64)
+    for j0 in range(0, g.n, gallery_chunk):
+        s = pairwise(qn, gn_all[j0:j0 + gallery_chunk].contiguous(), _lib.PW_DOT, 1.0, 0.0, torch.float64)
+        s = torch.nan_to_num(s, nan=float("-inf"))
+        cs, ci = torch.sort(s, dim=1, descending=True, stable=True)
+        cs, ci = cs[:, :k], ci[:, :k] + j0
+        # earlier chunks hold lower indices: [best | chunk] is index-ascending among equal scores
+        ms, mi = torch.cat([best_s, cs], 1), torch.cat([best_i, ci], 1)
+        o = torch.sort(ms, dim=1, descending=True, stable=True).indices[:, :k]
+        best_s, best_i = ms.gather(1, o), mi.gather(1, o)
+    return best_i.to(torch.int32), best_s
 
 
 def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):

@@ -67,10 +67,18 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const float* xr = x + row * ldx;
-  if constexpr (VEC4) {
+  if constexpr (VEC4) {  // chosen on the INPUT side only (ln_vec4_ok); the output may be unaligned
     float* yr = y + row * ldy;
+    const bool yvec = ((ldy & 3) == 0) && (((uintptr_t)y & 15) == 0);
     ln_row_vec4(xr, (int)d, gamma, beta, eps, [&](int j, float a, float b, float c, float e) {
-      reinterpret_cast<float4*>(yr)[j] = make_float4(a, b, c, e);
+      if (yvec) {
+        reinterpret_cast<float4*>(yr)[j] = make_float4(a, b, c, e);
+      } else {
+        yr[4 * j] = a;
+        yr[4 * j + 1] = b;
+        yr[4 * j + 2] = c;
+        yr[4 * j + 3] = e;
+      }
     });
     return;
   }
@@ -366,16 +374,21 @@ __global__ __launch_bounds__(256) void layernorm_pack_kernel(const float* __rest
     return;
   }
   const float* xr = x + row * ldx;
-  if constexpr (VEC4) {  // d_pad % 4 == 0: four bf16 per 8-byte store
+  if constexpr (VEC4) {  // chosen on the INPUT side only (ln_vec4_ok); 8-byte stores when the planes allow
+    const bool ovec = ((d_pad & 3) == 0) && (((uintptr_t)hi & 7) == 0) && (((uintptr_t)lo & 7) == 0);
     ln_row_vec4(xr, (int)d, gamma, beta, eps, [&](int j, float a, float b, float c, float e) {
       const uint16_t h0 = f2bf(a), h1 = f2bf(b), h2 = f2bf(c), h3 = f2bf(e);
-      reinterpret_cast<uint2*>(hr)[j] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
-      reinterpret_cast<uint2*>(lr)[j] =
-          make_uint2(f2bf(a - bf2f(h0)) | ((uint32_t)f2bf(b - bf2f(h1)) << 16),
-                     f2bf(c - bf2f(h2)) | ((uint32_t)f2bf(e - bf2f(h3)) << 16));
+      const uint16_t l0 = f2bf(a - bf2f(h0)), l1 = f2bf(b - bf2f(h1)), l2 = f2bf(c - bf2f(h2)),
+                     l3 = f2bf(e - bf2f(h3));
+      if (ovec) {
+        reinterpret_cast<uint2*>(hr)[j] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+        reinterpret_cast<uint2*>(lr)[j] = make_uint2(l0 | ((uint32_t)l1 << 16), l2 | ((uint32_t)l3 << 16));
+      } else {
+        hr[4 * j] = h0; hr[4 * j + 1] = h1; hr[4 * j + 2] = h2; hr[4 * j + 3] = h3;
+        lr[4 * j] = l0; lr[4 * j + 1] = l1; lr[4 * j + 2] = l2; lr[4 * j + 3] = l3;
+      }
     });
-    for (int64_t j = (d >> 2) + lane; j < (d_pad >> 2); j += 64)
-      reinterpret_cast<uint2*>(hr)[j] = reinterpret_cast<uint2*>(lr)[j] = make_uint2(0u, 0u);
+    for (int64_t k = d + lane; k < d_pad; k += 64) hr[k] = lr[k] = 0;
     return;
   }
   float v[16];
@@ -427,7 +440,8 @@ extern "C" int cmve_layernorm(cmve_handle_t h, const float* x, int64_t ldx, int6
   CMVE_REQUIRE(h && x && y, "cmve_layernorm: NULL argument");
   CMVE_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldy >= d, "cmve_layernorm: bad shape");
   if (n == 0) return CMVE_OK;
-  if (ln_vec4_ok(x, ldx, d, gamma, beta) && ldy % 4 == 0 && ((uintptr_t)y & 15) == 0)
+  // path chosen on the input side only, so cmve_layernorm and cmve_layernorm_pack sum in the same order
+  if (ln_vec4_ok(x, ldx, d, gamma, beta))
     hipLaunchKernelGGL(layernorm_kernel<true>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, h->stream, x, ldx, n, d,
                        gamma, beta, eps, y, ldy);
   else
@@ -540,8 +554,7 @@ extern "C" int cmve_layernorm_pack(cmve_handle_t h, const float* x, int64_t ldx,
   CMVE_REQUIRE(n >= 0 && d > 0 && d <= 1024 && ldx >= d, "cmve_layernorm_pack: bad shape (d <= 1024)");
   CMVE_REQUIRE(out->n == n && out->d == d && out->d_pad >= d && out->n_pad >= n, "cmve_layernorm_pack: bad out");
   if (out->n_pad) {
-    if (ln_vec4_ok(x, ldx, d, gamma, beta) && out->d_pad % 4 == 0 && ((uintptr_t)out->hi & 7) == 0 &&
-        ((uintptr_t)out->lo & 7) == 0)
+    if (ln_vec4_ok(x, ldx, d, gamma, beta))  // input side only (see cmve_layernorm)
       hipLaunchKernelGGL(layernorm_pack_kernel<true>, dim3((unsigned)((out->n_pad + 3) / 4)), dim3(256), 0, h->stream,
                          x, ldx, n, d, out->n_pad, out->d_pad, gamma, beta, eps, out->hi, out->lo);
     else

@@ -8,6 +8,7 @@
 //   SQ_L2   f = sum_k (a_k - b_k)^2              L2   f = sqrt(SQ_L2)
 //   L1      f = sum_k |a_k - b_k|                ORDER f = sqrt(sum_k max(0, b_k - a_k)^2)
 //   JACCARD f = sum_k min(a_k, b_k) / sum_k max(a_k, b_k)
+//   DOT     f = sum_k a_k b_k (k-ordered fp64 fma chain: the top-k's exact dense fallback)
 // No MFMA form exists for these reductions (min/max/abs per element): a VALU kernel with 64x128
 // output tiles per 256-thread block, 4x8 outputs per thread, K staged through LDS in 32-deep
 // slabs (converted to fp64 once on the way in), fp64 accumulation -- the reference's scipy path
@@ -34,6 +35,8 @@ __device__ __forceinline__ void pw_acc(double a, double b, double& s0, double& s
   } else if constexpr (METRIC == CMVE_PW_ORDER) {
     const double t = fmax(b - a, 0.0);
     s0 = fma(t, t, s0);
+  } else if constexpr (METRIC == CMVE_PW_DOT) {
+    s0 = fma(a, b, s0);
   } else {  // JACCARD
     s0 += fmin(a, b);
     s1 += fmax(a, b);
@@ -119,7 +122,7 @@ extern "C" int cmve_pairwise(cmve_handle_t h, const void* A, int32_t a_dtype, in
                              double beta, void* out, int32_t out_dtype, int64_t ldo) {
   CMVE_REQUIRE(h && A && B && out, "cmve_pairwise: NULL argument");
   CMVE_REQUIRE(na >= 0 && nb >= 0 && d > 0 && lda >= d && ldb >= d && ldo >= nb, "cmve_pairwise: bad shape");
-  CMVE_REQUIRE(metric >= CMVE_PW_SQ_L2 && metric <= CMVE_PW_JACCARD, "cmve_pairwise: unknown metric %d", metric);
+  CMVE_REQUIRE(metric >= CMVE_PW_SQ_L2 && metric <= CMVE_PW_DOT, "cmve_pairwise: unknown metric %d", metric);
   CMVE_REQUIRE((a_dtype == CMVE_F32 || a_dtype == CMVE_F64) && (b_dtype == CMVE_F32 || b_dtype == CMVE_F64) &&
                    (out_dtype == CMVE_F32 || out_dtype == CMVE_F64),
                "cmve_pairwise: dtypes must be CMVE_F32/CMVE_F64");
@@ -135,6 +138,7 @@ extern "C" int cmve_pairwise(cmve_handle_t h, const void* A, int32_t a_dtype, in
     case CMVE_PW_L2: PW_LAUNCH(TA, TB, TO, CMVE_PW_L2); break;         \
     case CMVE_PW_L1: PW_LAUNCH(TA, TB, TO, CMVE_PW_L1); break;         \
     case CMVE_PW_ORDER: PW_LAUNCH(TA, TB, TO, CMVE_PW_ORDER); break;   \
+    case CMVE_PW_DOT: PW_LAUNCH(TA, TB, TO, CMVE_PW_DOT); break;       \
     default: PW_LAUNCH(TA, TB, TO, CMVE_PW_JACCARD); break;            \
   }
 #define PW_OUT(TA, TB)              \

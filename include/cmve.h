@@ -460,11 +460,14 @@ int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g,
  *   CMVE_PW_SQ_L2   sum (a-b)^2          CMVE_PW_L2      sqrt(sum (a-b)^2)
  *   CMVE_PW_L1      sum |a-b|            CMVE_PW_ORDER   sqrt(sum max(0, b-a)^2)
  *   CMVE_PW_JACCARD sum min(a,b) / sum max(a,b)
+ *   CMVE_PW_DOT     sum a*b as a k-ordered fp64 fma chain (identical rows score identically: the
+ *                   exact dense fallback of the top-k, LINAS-engine/inference.py:78-79)
  * Replaces: LINAS-engine/evaluation.py:22-35,56-71 (scipy cdist 'euclidean' / 'minkowski' p=1,
  * l1_norm / l2_norm = -f/D - 1, -jaccard) and LINAS-engine/loss.py:13-73 (order_sim = -ORDER,
  * euclidean_sim / L2_sim = -SQ_L2, L1_sim = -L1, L1_sim_norm = L1/D - 1, L2_sim_norm = SQ_L2/D - 1,
  * jaccard_sim).  A, B: f32/f64 rows (device); out f32/f64 [na, nb] (device). */
-enum cmve_pw_metric { CMVE_PW_SQ_L2 = 0, CMVE_PW_L2 = 1, CMVE_PW_L1 = 2, CMVE_PW_ORDER = 3, CMVE_PW_JACCARD = 4 };
+enum cmve_pw_metric { CMVE_PW_SQ_L2 = 0, CMVE_PW_L2 = 1, CMVE_PW_L1 = 2, CMVE_PW_ORDER = 3, CMVE_PW_JACCARD = 4,
+                      CMVE_PW_DOT = 5 };
 int cmve_pairwise(cmve_handle_t h, const void* A, int32_t a_dtype, int64_t lda, int64_t na, const void* B,
                   int32_t b_dtype, int64_t ldb, int64_t nb, int64_t d, int32_t metric, double alpha, double beta,
                   void* out, int32_t out_dtype, int64_t ldo);

@@ -123,6 +123,14 @@ def test_gpu_layernorm_paths(d, strided):
                                   engine._ptr(ln.weight.detach()), engine._ptr(ln.bias.detach()), float(ln.eps),
                                   engine._ptr(ys), ys.stride(0)) == 0
         assert (ys - y).abs().max().item() < 1e-6
+    if d % 4 == 0 and d <= 1024:  # aligned input, misaligned output: the same (float4-row) sums, bit for bit
+        from cmve._lib import lib
+        ybig = torch.empty((z.shape[0], d + 3), dtype=torch.float32, device=z.device)
+        yo = ybig[:, 1:1 + d]
+        assert lib.cmve_layernorm(engine.handle(z.device), engine._ptr(z), z.stride(0), z.shape[0], d,
+                                  engine._ptr(ln.weight.detach()), engine._ptr(ln.bias.detach()), float(ln.eps),
+                                  engine._ptr(yo), yo.stride(0)) == 0
+        assert torch.equal(yo, y)
     z64 = z.double()
     ref = torch.nn.functional.layer_norm(z64, (d,), ln.weight.double(), ln.bias.double(), ln.eps)
     assert (y.double() - ref).abs().max().item() < 2e-6

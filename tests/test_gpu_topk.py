@@ -119,6 +119,25 @@ def test_topk_near_duplicates(torch_cuda):
     _check(idx, sc, s, 50)
 
 
+def test_topk_band_overflow_falls_back_to_exact(torch_cuda):
+    """More than TOPK_CAP (4096) gallery rows tie at the k-th score (exact duplicates) and no lo plane
+    for the split-bf16 retry: the dense fp64 fallback keeps the ids exact (ties by index)."""
+    from cmve import engine
+    rng = np.random.default_rng(22)
+    d = 256
+    gal = rng.standard_normal((20000, d))
+    base = rng.standard_normal(d)
+    dup = rng.choice(20000, 6000, replace=False)
+    gal[dup] = base
+    qs = np.stack([base + 0.3 * rng.standard_normal(d), rng.standard_normal(d)])
+    s = R.exact_scores64(qs, gal)
+    q = engine.RowSet(qs, with_lo=False)
+    g = engine.RowSet(gal, with_lo=False)
+    idx, sc = engine.topk(q, g, 10)
+    _check(idx, sc, s, 10)
+    assert set(idx[0]) <= set(dup.tolist())
+
+
 def test_gallery_scorer_ids(torch_cuda):
     """inference.py mirror: GalleryScorer.topk_ids == [video_ids[i] for i in argsort(cal_error)[:topK]]."""
     from cmve.linas.inference import GalleryScorer
