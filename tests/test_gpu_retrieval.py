@@ -274,8 +274,11 @@ def test_full_size_c3_against_independent_fp64(torch_cuda):
         exp_r[b:b + 2000] = 1 + (s > diag[b:b + 2000, None]).sum(dim=1).cpu().numpy()
         exp_c += (s > diag[None, :]).sum(dim=0).cpu().numpy()
     exp_c += 1
-    # ties / near-ties at 1e-13 could legitimately differ between two fp64 summation orders
-    assert (t2v != exp_r).sum() <= 2 and (v2t != exp_c).sum() <= 2
+    # bit-exact: two fp64 summation orders could only disagree on a pair within ~1e-16 of its GT score,
+    # which random data of this size does not produce (measured: 0 mismatches in either direction)
+    bad_r, bad_c = int((t2v != exp_r).sum()), int((v2t != exp_c).sum())
+    print(f"C3 full size: t2v mismatches {bad_r}, v2t mismatches {bad_c}, undecided pairs {ncand}")
+    assert bad_r == 0 and bad_c == 0, (np.nonzero(t2v != exp_r), np.nonzero(v2t != exp_c))
 
 
 @pytest.mark.parametrize("nq,ng,d,chunks", [(300, 5000, 256, 3), (64, 300, 100, 7), (257, 2049, 640, 2),
@@ -500,7 +503,8 @@ def test_bench_shape_ranks_against_independent_fp64(torch_cuda):
         sg = s.gather(1, gt[rows[b:b + 128]][:, None])
         exp[b:b + 128] = 1 + (s > sg).sum(dim=1).cpu().numpy()
     got = t2v[rows.cpu().numpy()]
-    assert (got != exp).sum() <= 1, np.nonzero(got != exp)
+    print(f"bench shape: {int((got != exp).sum())} mismatches of {got.size} sampled captions, {ncand} undecided pairs")
+    assert np.array_equal(got, exp), np.nonzero(got != exp)
 
 
 @pytest.mark.parametrize("nq,ng,d", [(3, 129, 100), (130, 257, 64), (1000, 1000, 1024), (257, 300, 1536),
