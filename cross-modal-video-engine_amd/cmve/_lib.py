@@ -31,6 +31,7 @@ PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD, PW_DOT = 0, 1, 2, 3, 4, 5
 PAIR_MSE, PAIR_SMOOTH_L1, PAIR_KL = 0, 1, 2
+ACT_RELU_K, ACT_SIGMOID_K, ACT_QUICKGELU_K = 0, 1, 2
 
 
 class Rows(C.Structure):
@@ -64,6 +65,15 @@ SIGNATURES = {
     "cmve_temporal_pool": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i32, _vp, _i64]),
     "cmve_pair_loss_fwd": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, C.c_float, _vp]),
     "cmve_pair_loss_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, C.c_float, _vp, _vp, _vp]),
+    "cmve_act_fwd": (C.c_int, [_vp, _vp, _i64, _i32, _vp]),
+    "cmve_act_bwd": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "cmve_layernorm_train_fwd": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, C.c_double, _vp, _i64, _vp, _vp]),
+    "cmve_layernorm_bwd": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "cmve_mha_1q_bwd": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64, _vp, _i64,
+                                  _vp, _i64]),
+    "cmve_combine_train_fwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
+    "cmve_combine_train_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    "cmve_pool_mean_bwd": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
     "cmve_adaptive_avg_pool2d": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "cmve_layernorm": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _i64]),
     "cmve_mha_1q": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64]),
@@ -125,7 +135,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 9
+#define CMVE_ABI_VERSION 10
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -516,6 +516,35 @@ int cmve_scale_multi(cmve_handle_t h, int32_t n, float* const* xs, const int64_t
 int cmve_adam_multi(cmve_handle_t h, int32_t n, float* const* params, float* const* grads, float* const* exp_avgs,
                     float* const* exp_avg_sqs, const int64_t* numels, const int64_t* steps, double lr, double beta1,
                     double beta2, double eps, double weight_decay, const float* grad_scale, int64_t* dev_step);
+
+/* ---- Combiner training step --------------------------------
+ * K16: MultiFusion/src/combiner_train.py:341-381 (combiner.train(); logits = combiner(ref, text, target);
+ * CE(logits, arange); backward; Adam) around cmve_gemm_f32(_ex) (Linear / 1x1 conv / in-projection
+ * GEMMs), K7 (CE) and K11 (dropout, Adam):
+ *   cmve_act_fwd / _bwd          kind 0 ReLU, 1 Sigmoid, 2 QuickGELU x*sigmoid(1.702x)
+ *                                (MultiFusion/src/combiner.py:8-9,104-105,151-176); bwd takes the INPUT x.
+ *   cmve_layernorm_train_fwd     LayerNorm rows (fp64 statistics), row mean / rstd saved (combiner.py:11-17)
+ *   cmve_layernorm_bwd           dx (nullable), dgamma / dbeta (nullable) from x, dy and the saved statistics
+ *   cmve_mha_1q_bwd              gradients of cmve_mha_1q (q, and K / V rows t*B + b of kv at columns 0 / v_off):
+ *                                softmax recomputed; dkv must not alias kv (combiner.py:38-43,164-165)
+ *   cmve_combine_train_fwd       out = ((y + ds*text) + (1-ds)*ref) + based, ds [B] (combiner.py:178-179)
+ *   cmve_combine_train_bwd       dtext = g ds, dref = g (1-ds), dds = sum_j g (text - ref) (outputs nullable)
+ *   cmve_pool_mean_bwd           dx[b, t, :] = dy[b, :] / T (time_process, combiner.py:140-143) */
+int cmve_act_fwd(cmve_handle_t h, const float* x, int64_t n, int32_t kind, float* y);
+int cmve_act_bwd(cmve_handle_t h, const float* x, const float* dy, int64_t n, int32_t kind, float* dx);
+int cmve_layernorm_train_fwd(cmve_handle_t h, const float* x, int64_t ldx, int64_t n, int64_t d, const float* gamma,
+                             const float* beta, double eps, float* y, int64_t ldy, float* save_mean, float* save_rstd);
+int cmve_layernorm_bwd(cmve_handle_t h, const float* x, int64_t ldx, const float* dy, int64_t lddy, int64_t n,
+                       int64_t d, const float* gamma, const float* save_mean, const float* save_rstd, float* dx,
+                       int64_t lddx, float* dgamma, float* dbeta);
+int cmve_mha_1q_bwd(cmve_handle_t h, const float* q, int64_t ldq, const float* kv, int64_t ldkv, int64_t v_off,
+                    int32_t B, int32_t T, int32_t H, int32_t dh, const float* dout, int64_t lddo, float* dq,
+                    int64_t lddq, float* dkv, int64_t lddkv);
+int cmve_combine_train_fwd(cmve_handle_t h, const float* y, const float* ds, const float* text, const float* ref,
+                           const float* based, int64_t B, int64_t d, float* out);
+int cmve_combine_train_bwd(cmve_handle_t h, const float* g, const float* ds, const float* text, const float* ref,
+                           int64_t B, int64_t d, float* dtext, float* dref, float* dds);
+int cmve_pool_mean_bwd(cmve_handle_t h, const float* dy, int64_t B, int64_t T, int64_t F, float* dx);
 
 /* ---- on-disk feature store -------------------------------
  * BigFile: feature.bin = n_rows x dim float32, row-major (LINAS-engine/basic/bigfile.py:6-18).

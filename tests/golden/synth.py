@@ -87,14 +87,29 @@ COMBINER_SHAPES = [
 ]
 
 
-def combiner_state(seed=11):
+def combiner_shapes(d, proj, hidden):
+    """COMBINER_SHAPES for Combiner(d, proj, hidden) (the same state-dict order)."""
+    sub = {640: d, 2560: proj, 5120: hidden, 1920: 3 * d}
+    out = []
+    for name, shape in COMBINER_SHAPES:
+        if name.startswith("self_attn_1.mlp"):  # the block's MLP is 4 * d wide, not proj
+            shape = tuple(4 * d if x == 2560 else d for x in shape)
+        else:
+            shape = tuple(sub.get(x, x) for x in shape)
+        out.append((name, shape))
+    return out
+
+
+def combiner_state(seed=11, dims=(640, 2560, 5120)):
     """Deterministic Combiner(640, 2560, 5120) weights (64.7M params) in state-dict order:
     weights ~ U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch's default Linear init range), biases
     ~ 0.05 N(0,1), LayerNorm gain 1 + 0.1 N(0,1).  Both the golden script (loading them into the
-    reference module) and the GPU test regenerate them, so no checkpoint is stored."""
+    reference module) and the GPU test regenerate them, so no checkpoint is stored.  ``dims`` =
+    (clip_feature_dim, projection_dim, hidden_dim) for a smaller Combiner."""
     rng = np.random.default_rng(seed)
     sd = {}
-    for name, shape in COMBINER_SHAPES:
+    shapes = COMBINER_SHAPES if tuple(dims) == (640, 2560, 5120) else combiner_shapes(*dims)
+    for name, shape in shapes:
         if name.endswith("ln_1.weight") or name.endswith("ln_2.weight"):
             v = 1.0 + 0.1 * rng.standard_normal(shape, dtype=np.float32)
         elif name.endswith("bias"):
