@@ -292,6 +292,7 @@ inline CandLayout cand_layout(int64_t g_n_pad, int64_t cap) {
   return l;
 }
 constexpr int64_t FIXUP_MAX_BUCKETS_PER_XCD = 4096;  // LDS prefix of the XCD-ordered fix-up
+constexpr int EVAL_EMAX_SHARDS = 64;  // K14: err_max shards per side and plane (eval.hip, sim.hip)
 
 // canonical exact score: cos64(x, y) = dot64(raw_x, raw_y) * (inv_x * inv_y), symmetric in (x, y), so
 // the GT-score, fix-up and top-k re-score kernels score a pair bit-identically
@@ -306,6 +307,8 @@ __device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double 
 // on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
 // PREFETCH: load the pair's GT scores before its dot product (latency-bound small evaluations; in the
 // bandwidth-bound bench-size fix-up that was 3% slower)
+// flat: one group over all buckets and every wave of the grid (small evaluations: a 1k-row gallery has
+// 4 buckets, which the XCD grouping would leave to 4 of the 8 XCDs); the caller keeps nb <= 4096
 template <typename TQ, typename TG, bool PREFETCH = false>
 __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -313,16 +316,17 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t nb, int64_t cap_b) {
+                                                    int64_t nb, int64_t cap_b, bool flat = false) {
   __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int xcd = blockIdx.x & 7;
-  const int64_t nk = xcd < nb ? (nb - xcd + 7) / 8 : 0;
+  const int G = flat ? 1 : 8;  // bucket groups (XCDs)
+  const int xcd = flat ? 0 : (blockIdx.x & 7);
+  const int64_t nk = xcd < nb ? (nb - xcd + G - 1) / G : 0;
   if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
     const int64_t per = (nk + 63) / 64;
     const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
     int64_t sum = 0;
-    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + 8 * k], cap_b);
+    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + G * k], cap_b);
     int64_t incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
       const int64_t t = __shfl_up(incl, o, 64);
@@ -331,18 +335,18 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
     int64_t run = incl - sum;
     for (int64_t k = k0; k < k1; ++k) {
       pre[k] = run;
-      run += min((int64_t)cand[xcd + 8 * k], cap_b);
+      run += min((int64_t)cand[xcd + G * k], cap_b);
     }
     if (lane == 63) pre[nk] = incl;
   }
   __syncthreads();
   const int64_t total = pre[nk];
   const int nw = (int)(blockDim.x >> 6);  // waves per block
-  const int64_t stride = (int64_t)(gridDim.x >> 3) * nw;
+  const int64_t stride = (int64_t)(gridDim.x / G) * nw;
   int64_t k = 0;
-  for (int64_t c = (int64_t)(blockIdx.x >> 3) * nw + wave; c < total; c += stride) {
+  for (int64_t c = (int64_t)(blockIdx.x / G) * nw + wave; c < total; c += stride) {
     while (pre[k + 1] <= c) ++k;
-    const uint64_t u = cand[nb + (xcd + 8 * k) * cap_b + (c - pre[k])];
+    const uint64_t u = cand[nb + (xcd + G * k) * cap_b + (c - pre[k])];
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     const uint32_t flags = (uint32_t)(u >> 62);

@@ -1,13 +1,18 @@
-// K14: one exact two-direction GT-rank evaluation of a resident problem in three launches
+// K14: one exact two-direction GT-rank evaluation of a resident problem in four launches
 // (cmve_eval_ranks, host side in sim.hip):
-//   1. eval_prep_kernel  K1 pack of BOTH sets, the exact fp64 GT score of every row of both
-//                        directions (K5a) and zeroed counters; the LAST block to finish derives the
-//                        sets' err_max and every rank threshold (agent-scope release / acquire
-//                        hand-off, cdna_hip_programming.md Guideline 16)
-//   2. sim_kernel<RANK>  K4 rank GEMM (certain counts + undecided pairs), unchanged
-//   3. eval_fix_kernel   K5b fp64 re-score of the undecided pairs; the LAST block turns the counts into
-//                        1-based ranks, R@1/5/10 + rank sums per direction, the pair total and the
-//                        overflow size
+//   1. eval_prep_kernel    K1 pack of BOTH sets, the exact fp64 GT score of every row of both
+//                          directions (K5a) and zeroed counters: one wave per row, 4 rows per block
+//                          (every CU busy), no tail; per-block err maxima into 16 atomic-max shards
+//   2. sim_kernel<RANK>    K4 rank GEMM (certain counts + undecided pairs); each block folds the other
+//                          set's err_max from the shards (scalar loads) and derives its rows' / columns'
+//                          thresholds from the GT scores itself (SimArgs::thr_gt)
+//   3. eval_fix_kernel     K5b fp64 re-score of the undecided pairs, 4 waves per block, no tail
+//   4. eval_finish_kernel  a block per 256 rows: the 1-based ranks, R@1/5/10 + rank sums per direction
+//                          (block sums added into the stats head); block 0 also the sets' err_max (from
+//                          the prep's shards), the pair total and the overflow size
+// Round 2 first ran this as three launches whose LAST blocks derived the thresholds and the ranks
+// (an agent-scope arrival hand-off): per-block stamps put ~5-6 us on each arrival chain and 4-7 us on
+// each one-block tail, against ~1 us per kernel boundary; the boundaries replace them.
 // It replaces the per-evaluation chain of the reference's validation / test loop
 // (LINAS-engine/validate.py:61-74, tester.py:133-139): evaluation.cal_error (evaluation.py:17-21,
 // both sets re-normalised, the full matrix in fp64) -> util/metrics.eval_q2m in both directions
@@ -18,79 +23,6 @@
 
 namespace cmve {
 
-__device__ __forceinline__ const float* side_err(const EvalSide& s, int mode) {
-  return mode == CMVE_SIM_BF16 ? s.err_hi : (mode == CMVE_SIM_BF16X3 ? s.err_hilo : s.err_h16);
-}
-
-// ---- in-launch hand-off to the last block (MI355X_MICROARCH.md "inter-workgroup visibility", valid form
-// "ONE lane of each storing workgroup ... agent-scope atomic add ... the workgroup whose add came last"):
-// the handed-off words are stored write-through (sc1: agent-scope relaxed atomic stores) or are agent
-// atomics, every wave waits for them (vmcnt(0)) before the block's barrier, one lane adds to the
-// arrival counter, and the last block reads them with sc1 loads behind one acquire.  No per-block L2
-// write-back (an agent release per block cost ~40 us over 512 blocks that had just dirtied the planes).
-typedef __attribute__((address_space(1))) unsigned gu32;
-typedef __attribute__((address_space(1))) int gi32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-// (integer atomics: ROCm 7.2 lowered a relaxed agent-scope atomic store of a float / double to a
-// plain global_store, without sc1)
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __builtin_bit_cast(double, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __builtin_bit_cast(float, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ int ld_sc1(const int* p) {
-  return __hip_atomic_load((gi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
-  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Arrival counting in two levels: block b adds to shard counter 1 + b % ARR_SHARDS (each on a line of
-// its own); the block completing a shard adds to the top counter 0, and the block completing the top
-// counter is the last.  One same-address atomic per block serialises at one L2 channel (~30 ns each:
-// 512 arrivals cost ~15 us), the shards take them in parallel.  Each block's handed-off words are
-// sc1 stores or agent atomics that completed (vmcnt(0)) before its add; the adds chain causally to
-// the last block, which reads them with sc1 loads behind one acquire.  The completing blocks reset the
-// counters they completed, so the words are zero again for the next launch (zeroed at allocation).
-constexpr int ARR_SHARDS = 8, ARR_STRIDE = 64;  // counters 256 B apart
-__device__ __forceinline__ bool last_block_arrival(unsigned* ctr_flat) {
-  __shared__ int s_last;
-  gu32* ctr = (gu32*)ctr_flat;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its sc1 stores / atomics have completed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned b = blockIdx.x, G = gridDim.x, sh = b % ARR_SHARDS;
-    const unsigned shard_size = (G - sh + ARR_SHARDS - 1) / ARR_SHARDS;
-    const unsigned shards = G < (unsigned)ARR_SHARDS ? G : (unsigned)ARR_SHARDS;
-    gu32* sc = ctr + ARR_STRIDE * (1 + sh);
-    int last = 0;
-    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shard_size - 1) {
-      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shards - 1) {
-        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = 1;
-      }
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return false;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return true;
-}
-
 // prep_row for rows of <= 1024 elements that both sides read in 16-B pieces (rows_vec4): the row is
 // loaded ONCE into registers (16 doubles per lane, elements 4L + 256m + c) and packed from there, and
 // each GT partner is read once for both its sum of squares and the dot product.  Every per-lane
@@ -100,7 +32,7 @@ __device__ __forceinline__ bool last_block_arrival(unsigned* ctr_flat) {
 template <typename TA, typename TB>
 __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide& B, const EvalCommon& c, int64_t row,
                                               const TA* __restrict__ x, uint16_t* hrow, uint16_t* lrow,
-                                              uint16_t* frow, int lane) {
+                                              uint16_t* frow, int lane, float (&eb)[3]) {
   double v[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -163,9 +95,12 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
   if (lane == 0) {
     A.inv[row] = inv;
     // pack_row_planes' bounds
-    st_sc1(&A.err_hi[row], bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY);
-    st_sc1(&A.err_hilo[row], bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY);
-    if (A.err_h16) st_sc1(&A.err_h16[row], f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12));
+    eb[0] = bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY;
+    eb[1] = bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY;
+    eb[2] = A.err_h16 ? f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12) : 0.f;
+    A.err_hi[row] = eb[0];
+    A.err_hilo[row] = eb[1];
+    if (A.err_h16) A.err_h16[row] = eb[2];
   }
   if (!A.off) return;
   double best = -INFINITY;
@@ -195,7 +130,7 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
     }
   }
   if (lane == 0) {
-    st_sc1(&A.sgt[row], any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN));
+    A.sgt[row] = any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN);
     A.cnt[row] = 0;
   }
 }
@@ -203,7 +138,7 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
 // pack row `row` of side A and score its GT list against side B (one wave)
 template <typename TA, typename TB>
 __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, const EvalCommon& c, int64_t row,
-                                         int lane) {
+                                         int lane, float (&eb)[3]) {
   uint16_t* hrow = A.hi + row * c.d_pad;
   uint16_t* lrow = A.lo ? A.lo + row * c.d_pad : nullptr;
   uint16_t* frow = A.h16 ? A.h16 + row * c.d_pad : nullptr;
@@ -211,11 +146,11 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
     pack_pad_row(hrow, lrow, frow, c.d_pad, lane);
     if (lane == 0) {
       A.inv[row] = 0.0;
-      st_sc1(&A.err_hi[row], 0.f);
-      st_sc1(&A.err_hilo[row], 0.f);
-      if (A.err_h16) st_sc1(&A.err_h16[row], 0.f);
+      A.err_hi[row] = 0.f;
+      A.err_hilo[row] = 0.f;
+      if (A.err_h16) A.err_h16[row] = 0.f;
       if (A.off) {
-        st_sc1(&A.sgt[row], (double)NAN);
+        A.sgt[row] = (double)NAN;
         A.cnt[row] = 0;
       }
     }
@@ -223,7 +158,7 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   }
   const TA* x = (const TA*)A.raw + row * A.ld;
   if (A.vec && B.vec && c.d_pad <= 1024) {
-    prep_row_regs<TA, TB>(A, B, c, row, x, hrow, lrow, frow, lane);
+    prep_row_regs<TA, TB>(A, B, c, row, x, hrow, lrow, frow, lane, eb);
     return;
   }
   const double inv = row_inv_norm(row_sumsq<TA>(x, c.d, A.vec != 0, lane), A.eps, A.flags);
@@ -231,9 +166,10 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   pack_row_planes<TA>(x, c.d, c.d_pad, A.vec != 0, inv, hrow, lrow, frow, lane, b1, b2, b3);
   if (lane == 0) {
     A.inv[row] = inv;
-    st_sc1(&A.err_hi[row], b1);  // handed to the last block (sc1): the rest only to later launches
-    st_sc1(&A.err_hilo[row], b2);
-    if (A.err_h16) st_sc1(&A.err_h16[row], b3);
+    A.err_hi[row] = eb[0] = b1;
+    A.err_hilo[row] = eb[1] = b2;
+    eb[2] = A.err_h16 ? b3 : 0.f;
+    if (A.err_h16) A.err_h16[row] = b3;
   }
   if (!A.off) return;
   // exact GT score (gt_thr_kernel's arithmetic): the partner's 1/||y|| is recomputed by the routine
@@ -252,19 +188,18 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   }
   if (lane == 0) {
     // empty list: NaN (rank n_m + 1); every GT NaN: +inf (rank n_m) -- gt_thr_kernel's encoding
-    st_sc1(&A.sgt[row], any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN));
+    A.sgt[row] = any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN);
     A.cnt[row] = 0;
   }
 }
 
-constexpr int EVAL_NT = 1024;  // threads per block of both kernels: the last block's tail covers a
-                               // 1k-row side in one pass
-constexpr int EVAL_NW = EVAL_NT / 64;
+constexpr int FIN_NT = 256;  // finish: 256 rows per block, one block per 256 rows of the larger side
+constexpr int FIN_NW = FIN_NT / 64;
 
-// reduce K values per thread over the block in ONE LDS round (max or sum); every thread gets the K
-// results in v (a reduction per value cost two barriers each: ~0.5 us per value in the tail)
+// reduce K values per thread over a block of FIN_NT threads in ONE LDS round (max or sum); every
+// thread gets the K results in v
 template <bool MAX, typename T, int K>
-__device__ __forceinline__ void block_reduce_k(T (&v)[K], T* red /* LDS [K + 1][EVAL_NW] */) {
+__device__ __forceinline__ void block_reduce_k(T (&v)[K], T* red /* LDS [K + 1][FIN_NW] */) {
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
@@ -274,14 +209,14 @@ __device__ __forceinline__ void block_reduce_k(T (&v)[K], T* red /* LDS [K + 1][
     }
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int k = 0; k < K; ++k) red[k * EVAL_NW + (threadIdx.x >> 6)] = v[k];
+    for (int k = 0; k < K; ++k) red[k * FIN_NW + (threadIdx.x >> 6)] = v[k];
   __syncthreads();
-  T* out = red + K * EVAL_NW;  // thread k < K folds row k (wave order: deterministic)
+  T* out = red + K * FIN_NW;  // thread k < K folds row k (wave order: deterministic)
   if (threadIdx.x < K) {
-    const T* r = red + threadIdx.x * EVAL_NW;
+    const T* r = red + threadIdx.x * FIN_NW;
     T a = r[0];
 #pragma unroll
-    for (int w = 1; w < EVAL_NW; ++w) a = MAX ? (r[w] > a ? r[w] : a) : a + r[w];
+    for (int w = 1; w < FIN_NW; ++w) a = MAX ? (r[w] > a ? r[w] : a) : a + r[w];
     out[threadIdx.x] = a;
   }
   __syncthreads();
@@ -289,174 +224,148 @@ __device__ __forceinline__ void block_reduce_k(T (&v)[K], T* red /* LDS [K + 1][
   for (int k = 0; k < K; ++k) v[k] = out[k];
 }
 
-// The last block of the prep launch: err_max of both sides (all three planes, real rows, NaN skipped:
-// err_max_kernel's result) and every rank threshold (gt_thr_kernel's).  Each pass issues all of a
-// thread's loads before using them (the tail runs on one CU: its latency is the launch's).
-__device__ __forceinline__ void prep_tail(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
-  __shared__ float red[7 * EVAL_NW];
-  float m[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-  const int64_t nmax = q.n > g.n ? q.n : g.n;
-  for (int64_t i = threadIdx.x; i < nmax; i += EVAL_NT) {
-    float e[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-    if (i < q.n) {
-      e[0][0] = ld_sc1(&q.err_hi[i]);
-      e[0][1] = ld_sc1(&q.err_hilo[i]);
-      if (q.err_h16) e[0][2] = ld_sc1(&q.err_h16[i]);
-    }
-    if (i < g.n) {
-      e[1][0] = ld_sc1(&g.err_hi[i]);
-      e[1][1] = ld_sc1(&g.err_hilo[i]);
-      if (g.err_h16) e[1][2] = ld_sc1(&g.err_h16[i]);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) m[s2][k] = fmaxf(m[s2][k], e[s2][k]);  // fmaxf drops a NaN operand
-  }
-  float mm[6] = {m[0][0], m[0][1], m[0][2], m[1][0], m[1][1], m[1][2]};
-  block_reduce_k<true>(mm, red);
-  if (threadIdx.x < 3) {
-    q.err_max[threadIdx.x] = mm[threadIdx.x];
-    g.err_max[threadIdx.x] = mm[3 + threadIdx.x];
-  }
-  const int slot = mode_slot(c.mode);
-  const float qmax = mm[slot], gmax = mm[3 + slot];
-  const float* qerr = side_err(q, c.mode);
-  const float* gerr = side_err(g, c.mode);
-  const int64_t pmax = q.n_pad > g.n_pad ? q.n_pad : g.n_pad;
-  for (int64_t r = threadIdx.x; r < pmax; r += EVAL_NT) {
-    const bool dq = q.off && r < q.n_pad, dg = g.off && r < g.n_pad;
-    double sq = 0.0, sg = 0.0;
-    float eq = 0.f, eg = 0.f;
-    if (dq) {
-      sq = ld_sc1(&q.sgt[r]);
-      eq = ld_sc1(&qerr[r]);
-    }
-    if (dg) {
-      sg = ld_sc1(&g.sgt[r]);
-      eg = ld_sc1(&gerr[r]);
-    }
-    // NaN (no GT, padding) or +inf (every GT NaN): never counted
-    if (dq) {
-      const double E = score_error_bound((double)eq, (double)gmax, c.d_pad, c.mode);
-      q.thr_hi[r] = sq < INFINITY ? f32_round_up(sq + E) : INFINITY;
-      q.thr_lo[r] = sq < INFINITY ? f32_round_down(sq - E) : INFINITY;
-    }
-    if (dg) {
-      const double E = score_error_bound((double)eg, (double)qmax, c.d_pad, c.mode);
-      g.thr_hi[r] = sg < INFINITY ? f32_round_up(sg + E) : INFINITY;
-      g.thr_lo[r] = sg < INFINITY ? f32_round_down(sg - E) : INFINITY;
-    }
-  }
-}
+constexpr int PREP_NT = 256;  // 4 rows per block: a 1k-A evaluation's 2,048 rows fill every CU
+constexpr int PREP_NW = PREP_NT / 64;
 
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(EVAL_NT) void eval_prep_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide g, EvalCommon c) {
   EVAL_STAMP(c, 0, 0);
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * EVAL_NW + (threadIdx.x >> 6);
-  for (int64_t t = (int64_t)blockIdx.x * EVAL_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * EVAL_NT)
+  const int64_t row = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
     c.bucket[t] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 10) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+  float eb[3] = {0.f, 0.f, 0.f};  // this wave's row bounds (lane 0; padding rows 0)
   if (!(c.dbg & 1)) {
     if (row < q.n_pad)
-      prep_row<TQ, TG>(q, g, c, row, lane);
+      prep_row<TQ, TG>(q, g, c, row, lane, eb);
     else if (row < q.n_pad + g.n_pad)
-      prep_row<TG, TQ>(g, q, c, row - q.n_pad, lane);
+      prep_row<TG, TQ>(g, q, c, row - q.n_pad, lane, eb);
+  }
+  // err_max shards: the block's max per plane (its 4 rows are one side: n_pad % 4 == 0), one atomic
+  // max on the float bits per plane into shard blockIdx % EMAX_SHARDS of its side (bounds are >= 0 or
+  // +inf; NaN dropped by fmaxf); 64 shards keep ~8 same-address atomics per shard for a 1k-A prep
+  // (16 shards: ~3 us of serialised atomics at the end of the launch).  The rank GEMM folds the shards of the mode's plane, the finish folds
+  // all of them into the sets' err_max and zeroes them for the next evaluation.
+  __shared__ float s_eb[PREP_NW][3];
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s_eb[threadIdx.x >> 6][k] = eb[k];
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float m = 0.f;
+#pragma unroll
+    for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
+    const int side = (int64_t)blockIdx.x * PREP_NW < q.n_pad ? 0 : 1;
+    unsigned* sh = &c.emax[(side * 3 + threadIdx.x) * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];
+    // +inf (a plane the mode does not write) is the largest value: a plain store equals the atomic max
+    if (m == INFINITY) *sh = __float_as_uint(m);
+    else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
   }
   EVAL_STAMP(c, 0, 1);
-  if (c.dbg & 2) return;
-  if (!last_block_arrival(c.done)) return;
-  EVAL_STAMP(c, 0, 2);
-  if (c.dbg & 4) return;
-  prep_tail(q, g, c);
-  EVAL_STAMP(c, 0, 3);
 }
 
-// The last block of the fix-up launch: pair total / overflow size (cand_finalize_kernel's), the ranks
-// of both directions (cmve_gt_ranks' rules) and per direction #rank<=1, <=5, <=10 and the rank sum.
-__device__ __forceinline__ void fix_tail(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
-  __shared__ unsigned long long red[10 * EVAL_NW];
-  __shared__ unsigned long long redm[2 * EVAL_NW];
-  unsigned long long tot = 0, mx = 0;
-  for (int64_t b = threadIdx.x; b < c.nb; b += EVAL_NT) {
-    const unsigned long long v = ld_sc1(&c.bucket[b]);
-    tot += v;
-    mx = v > mx ? v : mx;
-  }
-  unsigned long long acc[2][4] = {};
-  const int64_t nmax = q.n > g.n ? q.n : g.n;
-  for (int64_t i = threadIdx.x; i < nmax; i += EVAL_NT) {
-    const bool dq = q.off && i < q.n, dg = g.off && i < g.n;
-    int32_t cq = 0, cg = 0;
-    double sq = 0.0, sg = 0.0;
-    if (dq) {
-      cq = ld_sc1(&q.cnt[i]);  // agent atomics of this launch and the GEMM's
-      sq = q.sgt[i];           // written by an earlier launch
-    }
-    if (dg) {
-      cg = ld_sc1(&g.cnt[i]);
-      sg = g.sgt[i];
-    }
-    if (dq) {
-      const int64_t r = gt_rank_of(cq, sq, g.n);
-      q.ranks[i] = r;
-      acc[0][0] += (r <= 1);
-      acc[0][1] += (r <= 5);
-      acc[0][2] += (r <= 10);
-      acc[0][3] += (unsigned long long)r;
-    }
-    if (dg) {
-      const int64_t r = gt_rank_of(cg, sg, q.n);
-      g.ranks[i] = r;
-      acc[1][0] += (r <= 1);
-      acc[1][1] += (r <= 5);
-      acc[1][2] += (r <= 10);
-      acc[1][3] += (unsigned long long)r;
-    }
-  }
-  unsigned long long sums[9] = {acc[0][0], acc[0][1], acc[0][2], acc[0][3], acc[1][0], acc[1][1], acc[1][2],
-                                acc[1][3], tot};
-  unsigned long long mxs[1] = {mx};
-  block_reduce_k<false>(sums, red);
-  block_reduce_k<true>(mxs, redm);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < 4 ? q.off : g.off) c.stats[k] = (int64_t)sums[k];
-    c.stats[8] = (int64_t)sums[8];
-    c.stats[9] = (int64_t)mxs[0] > c.cap_b ? ((int64_t)mxs[0] + 1) * c.nb + c.nb + 1 : 0;
-  }
-}
+constexpr int FIX_NT = 256;
 
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(EVAL_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__global__ __launch_bounds__(FIX_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
   EVAL_STAMP(c, 2, 0);
   if (!(c.dbg & 8))
     fixup_walk<TQ, TG, true>((const TQ*)q.raw, q.ld, q.inv, (const TG*)g.raw, g.ld, g.inv, c.d, q.off ? q.sgt : nullptr,
-                       g.off ? g.sgt : nullptr, q.cnt, g.cnt, c.cand, c.nb, c.cap_b);
+                             g.off ? g.sgt : nullptr, q.cnt, g.cnt, c.cand, c.nb, c.cap_b,
+                             c.nb <= FIXUP_MAX_BUCKETS_PER_XCD);
   EVAL_STAMP(c, 2, 1);
-  if (c.dbg & 16) return;
-  if (!last_block_arrival(c.done + EVAL_ARRIVAL_WORDS)) return;
-  EVAL_STAMP(c, 2, 2);
+}
+
+// the pair total / overflow size (cand_finalize_kernel's), block 0
+__device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
+  __shared__ unsigned long long redt[2 * FIN_NW], redm[2 * FIN_NW];
+  unsigned long long tot[1] = {0}, mx[1] = {0};
+  for (int64_t b = threadIdx.x; b < c.nb; b += FIN_NT) {
+    const unsigned long long v = c.bucket[b];
+    tot[0] += v;
+    mx[0] = v > mx[0] ? v : mx[0];
+  }
+  block_reduce_k<false>(tot, redt);
+  block_reduce_k<true>(mx, redm);
+  if (threadIdx.x == 0) {
+    c.stats[8] = (int64_t)tot[0];
+    c.stats[9] = (int64_t)mx[0] > c.cap_b ? ((int64_t)mx[0] + 1) * c.nb + c.nb + 1 : 0;
+  }
+}
+
+// err_max of both sides (all three planes, real rows, NaN skipped: err_max_kernel's result) as
+// cmve_pack_rows leaves it, folded from the prep's shards, which are zeroed for the next evaluation
+// (the rank GEMM has read them); block 0
+__device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+  if (threadIdx.x < 6) {
+    unsigned m = 0u;
+    for (int k = 0; k < EMAX_SHARDS; ++k) m = max(m, c.emax[threadIdx.x * EMAX_SHARDS + k]);
+    const float* e = threadIdx.x < 3 ? q.err_max : g.err_max;
+    ((float*)e)[threadIdx.x % 3] = __uint_as_float(m);
+  }
+  __syncthreads();  // every fold has read the shards
+  for (int k = threadIdx.x; k < 6 * EMAX_SHARDS; k += FIN_NT) c.emax[k] = 0u;
+}
+
+// The ranks of both directions (cmve_gt_ranks' rules) for this block's 256 rows of each side and, per
+// direction, #rank<=1, <=5, <=10 and the rank sum, added into the stats head (zeroed by the prep)
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  EVAL_STAMP(c, 1, 0);
   if (c.dbg & 32) return;
-  fix_tail(q, g, c);
-  EVAL_STAMP(c, 2, 3);
+  __shared__ unsigned long long red[9 * FIN_NW];
+  if (blockIdx.x == 0) {
+    finish_buckets(c);
+    finish_err_max(q, g, c);
+  }
+  unsigned long long acc[8] = {};
+  const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
+  if (q.off && i < q.n) {
+    const int64_t r = gt_rank_of(q.cnt[i], q.sgt[i], g.n);
+    q.ranks[i] = r;
+    acc[0] = (r <= 1);
+    acc[1] = (r <= 5);
+    acc[2] = (r <= 10);
+    acc[3] = (unsigned long long)r;
+  }
+  if (g.off && i < g.n) {
+    const int64_t r = gt_rank_of(g.cnt[i], g.sgt[i], q.n);
+    g.ranks[i] = r;
+    acc[4] = (r <= 1);
+    acc[5] = (r <= 5);
+    acc[6] = (r <= 10);
+    acc[7] = (unsigned long long)r;
+  }
+  block_reduce_k<false>(acc, red);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if ((k < 4 ? q.off : g.off) && acc[k]) atomicAdd((unsigned long long*)&c.stats[k], acc[k]);
+  }
+  EVAL_STAMP(c, 1, 1);
 }
 
 template <typename TQ, typename TG>
 static int launch_eval_typed(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int phase, hipStream_t s) {
   if (phase == 0) {
-    const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + EVAL_NW - 1) / EVAL_NW);
-    hipLaunchKernelGGL((eval_prep_kernel<TQ, TG>), dim3(blocks), dim3(EVAL_NT), 0, s, q, g, c);
+    const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
+    hipLaunchKernelGGL((eval_prep_kernel<TQ, TG>), dim3(blocks), dim3(PREP_NT), 0, s, q, g, c);
     return check_launch("eval_prep_kernel");
   }
-  // 16 blocks of 16 waves per XCD: 2,048 waves for the few thousand undecided pairs of an evaluation
-  // of this size (the rank fix-up's grid is sized for millions of pairs)
-  hipLaunchKernelGGL((eval_fix_kernel<TQ, TG>), dim3(8u * 16u), dim3(EVAL_NT), 0, s, q, g, c);
-  return check_launch("eval_fix_kernel");
+  if (phase == 1) {
+    // 1,024 blocks of 4 waves, every wave one or two of the few thousand undecided pairs of an evaluation
+    // of this size, in one flat walk (the rank fix-up's grid is sized for millions of pairs)
+    hipLaunchKernelGGL((eval_fix_kernel<TQ, TG>), dim3(1024u), dim3(FIX_NT), 0, s, q, g, c);
+    return check_launch("eval_fix_kernel");
+  }
+  const int64_t nmax = q.n > g.n ? q.n : g.n;
+  hipLaunchKernelGGL((eval_finish_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT)), dim3(FIN_NT), 0, s,
+                     q, g, c);
+  return check_launch("eval_finish_kernel");
 }
 
-// phase 0: prep, phase 1: fix-up + ranks
+// phase 0: prep, phase 1: fix-up, phase 2: err_max + ranks + R@K
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s) {
   if (!q_f64 && !g_f64) return launch_eval_typed<float, float>(q, g, c, phase, s);

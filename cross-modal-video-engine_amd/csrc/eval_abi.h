@@ -4,7 +4,8 @@
 
 namespace cmve {
 
-constexpr int EVAL_ARRIVAL_WORDS = 9 * 64;  // top + 8 shard counters, 256 B apart (eval.hip)
+constexpr int EVAL_ARRIVAL_WORDS = 9 * 64;  // workspace words zeroed at allocation: the err_max shards
+constexpr int EMAX_SHARDS = EVAL_EMAX_SHARDS;  // per side and plane: [side][plane][shard] float bits
 
 // one side of the problem: a packed set and the GT lists of the direction whose queries are its rows
 struct EvalSide {
@@ -34,21 +35,22 @@ struct EvalSide {
 struct EvalCommon {
   int64_t d, d_pad;
   int mode;
-  unsigned* done;              // arrival counters: prep at [0, EVAL_ARRIVAL_WORDS), fix-up after them
-                               // (self-resetting, zero at allocation)
+  unsigned* emax;              // err_max shards [2][3][EMAX_SHARDS] (float bits; zero at allocation, re-zeroed
+                               // by every evaluation's finish)
   unsigned long long* bucket;  // bucket counters at the head of the undecided-pair buffer
   int64_t nb, cap_b;
   const uint64_t* cand;
   int64_t* stats;              // out[0, 16)
   int dbg;                     // kernel studies only (CMVE_EVAL_DBG): skip parts, results garbage
-  unsigned long long* stamps;  // kernel studies only (CMVE_EVAL_DBG & 128): [kernel][block][4] s_memrealtime
+  unsigned long long* stamps;  // kernel studies only (CMVE_EVAL_DBG & 128): [kernel][block][8] s_memrealtime
+                               // (kernel 0 prep, 1 finish, 2 fix-up, 3 the rank GEMM's tiles)
 };
 
-// phase 0: pack + GT scores + thresholds, phase 1: fix-up + ranks (phase 2 is the rank GEMM, sim.hip)
-// stamp k of block b in kernel kern (0 prep, 1 rank GEMM, 2 fix-up) when stamps are on
+// phase 0: pack + GT scores, phase 1: fix-up, phase 2: err_max + ranks + R@K (the rank GEMM runs between
+// phases 0 and 1, sim.hip); stamp k of block b in kernel kern (0 prep, 1 finish, 2 fix-up) when stamps are on
 #define EVAL_STAMP(cp, kern, k)                                                                                  \
   if ((cp).stamps && threadIdx.x == 0)                                                                           \
-  (cp).stamps[((size_t)(kern) * 1024 + blockIdx.x) * 4 + (k)] = __builtin_amdgcn_s_memrealtime()
+  (cp).stamps[((size_t)(kern) * 1024 + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s);
 

@@ -69,6 +69,17 @@ struct SimArgs {
   unsigned long long* cand_count;
   unsigned long long* bucket_cnt;  // per-bucket pair counters (head of the caller's buffer)
   long long cap_b;
+  // rank thresholds derived in-kernel from the exact GT scores (K14): thr = dir-rounded sgt +- E(e_row,
+  // err_max of the other set), the err_max reduced from the other set's per-row bounds at kernel start;
+  // replaces row_hi / row_lo / col_hi / col_lo (which then only say which directions are on)
+  int thr_gt;
+  const double* row_sgt;
+  const double* col_sgt;
+  const float* q_err;  // per-row bounds of the mode's plane, [n_pad] (padding rows 0)
+  const float* g_err;
+  const unsigned* q_emax;  // err_max shards of the mode's plane, [EMAX_SHARDS] float bits each side
+  const unsigned* g_emax;
+  unsigned long long* dbg_stamps;  // kernel studies only: [tile][8] stamps, nullptr otherwise
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
@@ -186,11 +197,21 @@ constexpr size_t stage_bytes() {
   return (size_t)((MODE == CMVE_SIM_BF16X3 && !PHASED) ? 2 : 1) * (BM + BN) * BK * 2;
 }
 
+// staging ring depth of the 2-stage (non-phased) loop: the G64 tiles of small problems keep NS - 1
+// K-tiles in flight (a 1k x 1k x 1024 GEMM is latency-bound: with 2 stages every one of its 16 K-tiles
+// exposed a full L2 / Infinity-Cache round trip, ~1.2 us each against ~0.1 us of MFMAs); the vmcnt
+// immediate (<= 63) caps it for split-bf16, whose stages carry twice the loads
+template <int MODE, int BM, int BN, bool PHASED>
+constexpr int ring_stages() {
+  return (PHASED || BM != 64 || BN != 64) ? 2 : (MODE == CMVE_SIM_BF16X3 ? 4 : 8);
+}
+
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
 #define CMVE_STAMP(k) \
   if (threadIdx.x == 0) a.bucket_cnt[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memtime()
-#else
-#define CMVE_STAMP(k)
+#else  // kernel studies of the K14 evaluation (CMVE_EVAL_DBG & 128): s_memrealtime into SimArgs::dbg_stamps
+#define CMVE_STAMP(k) \
+  if (a.dbg_stamps && threadIdx.x == 0) a.dbg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
 #endif
 
 // Split-bf16 (BF16X3) in the phased G256 loop: ONE bf16 GEMM over K' = 3K whose K'-tile 3t + p
@@ -231,6 +252,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED>();
+  constexpr int NS = ring_stages<MODE, BM, BN, PHASED>();
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -262,16 +284,42 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   float thr_hi_v = __builtin_nanf(""), thr_lo_v = __builtin_nanf("");
   // a tile's thresholds are fetched when its loads are issued and published to LDS in its
   // epilogue: the epilogue must not wait on HBM (8 dependent loads per wave there cost ~28%)
+  // K14: the other set's err_max, folded once per block from the prep's shards (the max over real rows
+  // of the per-row bounds, NaN dropped, as err_max_kernel computes it); the thresholds then follow
+  // gt_thr_kernel's rule per row / column
+  float qmax_v = 0.f, gmax_v = 0.f;
+  auto reduce_err_max = [&]() {  // fold the prep's err_max shards (uniform addresses: scalar loads)
+    unsigned mq = 0u, mg = 0u;
+#pragma unroll
+    for (int k = 0; k < EVAL_EMAX_SHARDS; ++k) {
+      mq = max(mq, a.q_emax[k]);
+      mg = max(mg, a.g_emax[k]);
+    }
+    qmax_v = __uint_as_float(mq);
+    gmax_v = __uint_as_float(mg);
+  };
+  auto thr_of = [&](double sgt, float e, float emax_other, float& hi, float& lo) {
+    // NaN (no GT, padding) or +inf (every GT NaN): never counted
+    const double E = score_error_bound((double)e, (double)emax_other, a.ldk, MODE);
+    hi = sgt < INFINITY ? f32_round_up(sgt + E) : INFINITY;
+    lo = sgt < INFINITY ? f32_round_down(sgt - E) : INFINITY;
+  };
   auto fetch_thr = [&](int mo, int no, float& hi, float& lo) {
     hi = lo = __builtin_nanf("");
     if (tid < BM) {
       if (a.row_hi) {
-        hi = a.row_hi[mo + tid];
-        lo = a.row_lo[mo + tid];
+        if (a.thr_gt) thr_of(a.row_sgt[mo + tid], a.q_err[mo + tid], gmax_v, hi, lo);
+        else {
+          hi = a.row_hi[mo + tid];
+          lo = a.row_lo[mo + tid];
+        }
       }
     } else if (a.col_hi) {
-      hi = a.col_hi[no + tid - BM];
-      lo = a.col_lo[no + tid - BM];
+      if (a.thr_gt) thr_of(a.col_sgt[no + tid - BM], a.g_err[no + tid - BM], qmax_v, hi, lo);
+      else {
+        hi = a.col_hi[no + tid - BM];
+        lo = a.col_lo[no + tid - BM];
+      }
     }
   };
   // EPI_BIAS / EPI_LINEAR: the tile's bias (and BN) columns are fetched with its loads too
@@ -294,7 +342,12 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   if constexpr (epi_thr(EPI)) {
     static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
-    fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+    // K14 thresholds need the block's err_max reduction first: the 2-stage loop does both after issuing
+    // its first loads (below), the persistent loop here
+    if (PHASED || !a.thr_gt) {
+      if (a.thr_gt) reduce_err_max();
+      fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+    }
   }
 
   auto stage = [&](int t, int s) {
@@ -774,8 +827,92 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
 #undef CMVE_BAR
+  } else if constexpr (NS > 2) {
+  // ---- ring of NS stages (G64): K-tiles t+1 .. t+NS-2 stay in flight while K-tile t is consumed ----
+  constexpr int LPS = (BM / 8 / NW + BN / 8 / NW) * (MODE == CMVE_SIM_BF16X3 ? 2 : 1);  // loads / stage / wave
+  static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
+  const int nk0 = a.nk0;
+  for (int t = 0; t < NS - 1 && t < nk0; ++t) stage(t, t);
+  if constexpr (epi_thr(EPI)) {
+    if (a.thr_gt) {  // overlaps the first K-tiles' loads
+      reduce_err_max();
+      fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+    }
+  }
+  CMVE_STAMP(1);
+  for (int t = 0; t < nk0; ++t) {
+    // K-tile t has landed once at most LPS * (newer stages in flight) loads of this wave are outstanding
+    const int newer = min(NS - 2, nk0 - 1 - t);
+    switch (newer) {
+#define CMVE_RING_WAIT(k) \
+  case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS * (k)) : "memory"); break;
+      CMVE_RING_WAIT(0) CMVE_RING_WAIT(1) CMVE_RING_WAIT(2) CMVE_RING_WAIT(3) CMVE_RING_WAIT(4) CMVE_RING_WAIT(5)
+      CMVE_RING_WAIT(6)
+#undef CMVE_RING_WAIT
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // every wave's share of K-tile t is in LDS, every wave is done with K-tile t-1 (an LDS-only barrier:
+    // __syncthreads would drain vmcnt, i.e. the ring)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + NS - 1 < nk0) stage(t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
+    const char* base = smem + (t % NS) * STAGE_BYTES;
+    const char* pA = base;
+    const char* pB = base + A_BYTES;
+    s16x8_t fa[2][TM], fb[2][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[ks][j] = read_frag(pB, wc * (TN * 16) + j * 16 + frow, chunk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag(pA, wr * (TM * 16) + i * 16 + frow, chunk);
+    }
+    if constexpr (MODE == CMVE_SIM_BF16X3) {  // pairs (lo, hi) then (hi, lo): plane_of's order
+      const char* pAl = base + A_BYTES + B_BYTES;
+      const char* pBl = base + 2 * A_BYTES + B_BYTES;
+      s16x8_t lx[2][TM > TN ? TM : TN];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) lx[ks][i] = read_frag(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(lx[ks][i], fb[ks][j], acc[i][j]);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) lx[ks][j] = read_frag(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], lx[ks][j], acc[i][j]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the threshold loads, if any are still out)
+  CMVE_STAMP(2);
   } else {
   stage(0, 0);
+  if constexpr (epi_thr(EPI)) {
+    if (a.thr_gt) {  // overlaps the first K-tile's loads
+      reduce_err_max();
+      fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -854,7 +991,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = 2 * stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
+  const size_t lds = ring_stages<MODE, G::BM, G::BN, PHASED>() *
+                     stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
   static bool attr_done = false;
   if (!attr_done) {
     CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
@@ -884,7 +1022,7 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
 }
 
 // G256 (phased schedule) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
-// tiles; else G128 (2-stage).  CMVE_SIM_GEO=128 / 2562 force G128 / the 2-stage G256 loop
+// tiles; G64 below 128 tiles of 128^2; else G128 (2-stage).  CMVE_SIM_GEO=128 / 2562 force G128 / the 2-stage G256 loop
 // (kernel studies only).
 template <int MODE, int EPI>
 static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
@@ -897,6 +1035,10 @@ static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStrea
       if (force == 2562) return launch_geo<MODE, EPI, 2, 4, 8, false>(a, nq_pad, ng_pad, stream);  // 2-stage BK64
     return launch_geo<MODE, EPI, 2, 4, 8, true>(a, nq_pad, ng_pad, stream);
   }
+  // G64 (2 waves, 64 x 64 tiles) when the 128^2 grid would leave most CUs idle (a 1k x 1k problem: 64
+  // tiles of 128^2 vs 256 of 64^2); every output element sees the same MFMA sequence in every geometry
+  if (force != 128 && (nq_pad / 128) * (ng_pad / 128) < 128 && nq_pad % 64 == 0 && ng_pad % 64 == 0)
+    return launch_geo<MODE, EPI, 2, 1, 2, false>(a, nq_pad, ng_pad, stream);
   return launch_geo<MODE, EPI, 2, 2, 4, false>(a, nq_pad, ng_pad, stream);
 }
 
@@ -1246,7 +1388,7 @@ static unsigned long long* g_eval_stamps = nullptr;
 extern "C" int cmve_eval_debug_stamps(void* host, int64_t bytes) {
   CMVE_REQUIRE(g_eval_stamps && host, "cmve_eval_debug_stamps: no stamps (CMVE_EVAL_DBG & 128)");
   CMVE_HIP(hipDeviceSynchronize());
-  CMVE_HIP(hipMemcpy(host, g_eval_stamps, std::min<int64_t>(bytes, sizeof(unsigned long long) * 3 * 1024 * 4),
+  CMVE_HIP(hipMemcpy(host, g_eval_stamps, std::min<int64_t>(bytes, sizeof(unsigned long long) * 4 * 1024 * 8),
                      hipMemcpyDeviceToHost));
   return CMVE_OK;
 }
@@ -1315,6 +1457,8 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   const CandLayout l = cand_layout(g->n_pad, cand_cap);
   CMVE_REQUIRE(l.cap_b > 0, "cmve_eval_ranks: cand_cap %lld cannot hold the %lld bucket counters", (long long)cand_cap,
                (long long)l.nb);
+  CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "cmve_eval_ranks: gallery set too large (%lld buckets)",
+               (long long)l.nb);
   hipEvent_t* ev = nullptr;
   if (timing_slot >= 0) {
     ev = h->eval_ev[timing_slot];
@@ -1329,7 +1473,7 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   c.d = q->d;
   c.d_pad = q->d_pad;
   c.mode = mode;
-  c.done = (unsigned*)(base + w.done);
+  c.emax = (unsigned*)(base + w.done);
   uint64_t* cand = (uint64_t*)(base + w.cand);
   c.bucket = (unsigned long long*)cand;
   c.nb = l.nb;
@@ -1342,7 +1486,10 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   }();
   c.dbg = dbg;
   static unsigned long long* stamp_buf = nullptr;
-  if ((dbg & 128) && !stamp_buf) CMVE_HIP(hipMalloc(&stamp_buf, sizeof(unsigned long long) * 3 * 1024 * 4));
+  if ((dbg & 128) && !stamp_buf) {
+    CMVE_HIP(hipMalloc(&stamp_buf, sizeof(unsigned long long) * 4 * 1024 * 8));
+    CMVE_HIP(hipMemset(stamp_buf, 0, sizeof(unsigned long long) * 4 * 1024 * 8));
+  }
   c.stamps = (dbg & 128) ? stamp_buf : nullptr;
   g_eval_stamps = c.stamps;
   const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
@@ -1352,21 +1499,33 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
   SimArgs a = make_args(q, g, mode);
+  // thresholds derived in the GEMM from the prep's GT scores and per-row bounds (row_hi / col_hi only
+  // mark the directions that are on)
+  a.thr_gt = 1;
+  a.q_err = mode_err(q, mode);
+  a.g_err = mode_err(g, mode);
+  a.q_emax = c.emax + (0 * 3 + mode_slot(mode)) * cmve::EMAX_SHARDS;
+  a.g_emax = c.emax + (1 * 3 + mode_slot(mode)) * cmve::EMAX_SHARDS;
   if (row_off) {
     a.row_hi = sq.thr_hi;
     a.row_lo = sq.thr_lo;
+    a.row_sgt = sq.sgt;
     a.row_cnt = sq.cnt;
   }
   if (col_off) {
     a.col_hi = sg.thr_hi;
     a.col_lo = sg.thr_lo;
+    a.col_sgt = sg.sgt;
     a.col_cnt = sg.cnt;
   }
   set_cand(a, g, cand, cand_cap, out + 10);  // (the epilogue never writes cand_count)
+  a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
   st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
+  if (st) return st;
+  st = cmve::launch_eval(sq, sg, c, qf, gf, 2, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
   return CMVE_OK;
