@@ -325,19 +325,39 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
   if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
     const int64_t per = (nk + 63) / 64;
     const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
-    int64_t sum = 0;
-    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + G * k], cap_b);
-    int64_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
+    if (per <= 4) {  // (<= 256 buckets: one round of loads held in registers)
+      int64_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (k0 + j < k1) ? min((int64_t)cand[xcd + G * (k0 + j)], cap_b) : 0;
+      const int64_t sum = (v[0] + v[1]) + (v[2] + v[3]);
+      int64_t incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      int64_t run = incl - sum;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (k0 + j < k1) {
+          pre[k0 + j] = run;
+          run += v[j];
+        }
+      if (lane == 63) pre[nk] = incl;
+    } else {
+      int64_t sum = 0;
+      for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + G * k], cap_b);
+      int64_t incl = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      int64_t run = incl - sum;
+      for (int64_t k = k0; k < k1; ++k) {
+        pre[k] = run;
+        run += min((int64_t)cand[xcd + G * k], cap_b);
+      }
+      if (lane == 63) pre[nk] = incl;
     }
-    int64_t run = incl - sum;
-    for (int64_t k = k0; k < k1; ++k) {
-      pre[k] = run;
-      run += min((int64_t)cand[xcd + G * k], cap_b);
-    }
-    if (lane == 63) pre[nk] = incl;
   }
   __syncthreads();
   const int64_t total = pre[nk];
@@ -345,7 +365,15 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
   const int64_t stride = (int64_t)(gridDim.x / G) * nw;
   int64_t k = 0;
   for (int64_t c = (int64_t)(blockIdx.x / G) * nw + wave; c < total; c += stride) {
-    while (pre[k + 1] <= c) ++k;
+    if (pre[k + 1] <= c) {  // the bucket holding pair c: binary search of the prefix (the flat walk of
+      int64_t lo = k + 1, hi = nk - 1;  // a 256-bucket evaluation would scan up to 256 LDS words)
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= c) lo = mid;
+        else hi = mid - 1;
+      }
+      k = lo;
+    }
     const uint64_t u = cand[nb + (xcd + G * k) * cap_b + (c - pre[k])];
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);

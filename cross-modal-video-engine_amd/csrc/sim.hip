@@ -80,6 +80,10 @@ struct SimArgs {
   const unsigned* q_emax;  // err_max shards of the mode's plane, [EMAX_SHARDS] float bits each side
   const unsigned* g_emax;
   unsigned long long* dbg_stamps;  // kernel studies only: [tile][8] stamps, nullptr otherwise
+  // K14: undecided pairs bucketed by 64 x 64 output tile (bucket (m0 >> 6) * nbn64 + (n0 >> 6)) instead of by
+  // 256 gallery rows: a 1k x 1k evaluation otherwise sends every wave's slot reservation to one of 4 counters
+  int tile_buckets;
+  int nbn64;
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
@@ -599,7 +603,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         }
       }
       // a tile never straddles buckets (BM, BN <= 256, aligned)
-      const int bucket = EPI == EPI_TOPK ? (m0 >> 8) : (n0 >> CAND_BUCKET_SHIFT);
+      const int bucket = EPI == EPI_TOPK ? (m0 >> 8)
+                                         : (a.tile_buckets ? (m0 >> 6) * a.nbn64 + (n0 >> 6) : (n0 >> CAND_BUCKET_SHIFT));
       unsigned long long wbase = 0ull;
       if (total && lane == 0) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
       CMVE_STAMP(6);
@@ -1454,7 +1459,16 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   const EvalWs w = eval_ws_layout(q->n_pad, g->n_pad, cand_cap);
   CMVE_REQUIRE(cand_cap > 0 && ws_bytes >= (int64_t)w.total, "cmve_eval_ranks: workspace has %lld bytes, needs %lld",
                (long long)ws_bytes, (long long)w.total);
-  const CandLayout l = cand_layout(g->n_pad, cand_cap);
+  CandLayout l = cand_layout(g->n_pad, cand_cap);
+  // one bucket per 64 x 64 output tile when the grid is small: each wave reserves its undecided-pair
+  // slots on its own tile's counter (by 256 gallery rows a 1k x 1k evaluation has 4 counters, ~125
+  // serialised returning atomics each); the fix-up walks them flat
+  const int64_t nb_tiles = (q->n_pad >> 6) * (g->n_pad >> 6);
+  const bool tile_buckets = nb_tiles <= FIXUP_MAX_BUCKETS_PER_XCD && cand_cap >= 8 * nb_tiles;
+  if (tile_buckets) {
+    l.nb = nb_tiles;
+    l.cap_b = (cand_cap - nb_tiles) / nb_tiles;
+  }
   CMVE_REQUIRE(l.cap_b > 0, "cmve_eval_ranks: cand_cap %lld cannot hold the %lld bucket counters", (long long)cand_cap,
                (long long)l.nb);
   CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "cmve_eval_ranks: gallery set too large (%lld buckets)",
@@ -1519,6 +1533,11 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     a.col_cnt = sg.cnt;
   }
   set_cand(a, g, cand, cand_cap, out + 10);  // (the epilogue never writes cand_count)
+  a.bucket_cnt = (unsigned long long*)cand;  // the evaluation's layout (l: per-tile buckets when small)
+  a.cand = (unsigned long long*)(cand + l.nb);
+  a.cap_b = l.cap_b;
+  a.tile_buckets = tile_buckets;
+  a.nbn64 = (int)(g->n_pad >> 6);
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
