@@ -214,8 +214,12 @@ constexpr int ring_stages() {
 #define CMVE_STAMP(k) \
   if (threadIdx.x == 0) a.bucket_cnt[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memtime()
 #else  // kernel studies of the K14 evaluation (CMVE_EVAL_DBG & 128): s_memrealtime into SimArgs::dbg_stamps
+// (the 2-stage / ring loops only: the persistent G256 kernel is compiled without them -- the extra
+// scalar branches and stores cost it SGPR spills at the 256-VGPR cap)
 #define CMVE_STAMP(k) \
-  if (a.dbg_stamps && threadIdx.x == 0) a.dbg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+  if constexpr (!PHASED) {  \
+    if (a.dbg_stamps && threadIdx.x == 0) a.dbg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  }
 #endif
 
 // Split-bf16 (BF16X3) in the phased G256 loop: ONE bf16 GEMM over K' = 3K whose K'-tile 3t + p
@@ -312,14 +316,14 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     hi = lo = __builtin_nanf("");
     if (tid < BM) {
       if (a.row_hi) {
-        if (a.thr_gt) thr_of(a.row_sgt[mo + tid], a.q_err[mo + tid], gmax_v, hi, lo);
+        if (!PHASED && a.thr_gt) thr_of(a.row_sgt[mo + tid], a.q_err[mo + tid], gmax_v, hi, lo);
         else {
           hi = a.row_hi[mo + tid];
           lo = a.row_lo[mo + tid];
         }
       }
     } else if (a.col_hi) {
-      if (a.thr_gt) thr_of(a.col_sgt[no + tid - BM], a.g_err[no + tid - BM], qmax_v, hi, lo);
+      if (!PHASED && a.thr_gt) thr_of(a.col_sgt[no + tid - BM], a.g_err[no + tid - BM], qmax_v, hi, lo);
       else {
         hi = a.col_hi[no + tid - BM];
         lo = a.col_lo[no + tid - BM];
@@ -346,12 +350,11 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   if constexpr (epi_thr(EPI)) {
     static_assert(NT == BM + BN, "one threshold pair per thread");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
-    // K14 thresholds need the block's err_max reduction first: the 2-stage loop does both after issuing
-    // its first loads (below), the persistent loop here
-    if (PHASED || !a.thr_gt) {
-      if (a.thr_gt) reduce_err_max();
-      fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
-    }
+    // K14 thresholds need the block's err_max reduction first: the 2-stage / ring loops do both after
+    // issuing their first loads (below).  The persistent G256 kernel never derives them (cmve_eval_ranks
+    // writes them with eval_thr_kernel first): the derivation's code alone cost it 18% (SGPR spills at
+    // the 256-VGPR cap, 3.86 -> 4.56 ms at 16,384 x 131,072)
+    if (PHASED || !a.thr_gt) fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
   }
 
   auto stage = [&](int t, int s) {
@@ -1029,12 +1032,24 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
 // G256 (phased schedule) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
 // tiles; G64 below 128 tiles of 128^2; else G128 (2-stage).  CMVE_SIM_GEO=128 / 2562 force G128 / the 2-stage G256 loop
 // (kernel studies only).
-template <int MODE, int EPI>
-static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
+static int sim_geo_force() {
   static const int force = [] {
     const char* e = getenv("CMVE_SIM_GEO");
     return e ? atoi(e) : 0;
   }();
+  return force;
+}
+
+// true when launch_sim takes the persistent phased G256 kernel (which reads explicit thresholds only)
+static bool sim_uses_phased(int mode, int64_t nq_pad, int64_t ng_pad) {
+  const int force = sim_geo_force();
+  if (force == 128 || nq_pad % 256 || ng_pad % 256 || (nq_pad / 256) * (ng_pad / 256) < 512) return false;
+  return !(force == 2562 && mode != CMVE_SIM_BF16X3);
+}
+
+template <int MODE, int EPI>
+static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
+  const int force = sim_geo_force();
   if (force != 128 && nq_pad % 256 == 0 && ng_pad % 256 == 0 && (nq_pad / 256) * (ng_pad / 256) >= 512) {
     if constexpr (MODE != CMVE_SIM_BF16X3)  // (split-bf16 takes the phased loop only)
       if (force == 2562) return launch_geo<MODE, EPI, 2, 4, 8, false>(a, nq_pad, ng_pad, stream);  // 2-stage BK64
@@ -1434,6 +1449,31 @@ static cmve::EvalSide eval_side(cmve_rows_t* r, const int64_t* off, const int32_
   return s;
 }
 
+// K14 at G256 sizes: the persistent rank kernel reads explicit thresholds, so they are written here by
+// the rule the 2-stage / ring kernels apply in-kernel (sim_kernel's thr_of: the other set's err_max
+// folded from the prep's shards, then gt_thr_kernel's directed rounding); one thread per row of either set
+struct EvalThrSide {
+  const double* sgt;
+  const float* err;
+  const unsigned* emax_other;
+  float* hi;
+  float* lo;
+  int64_t n_pad;
+};
+__global__ __launch_bounds__(256) void eval_thr_kernel(EvalThrSide s0, EvalThrSide s1, int64_t d_pad, int mode) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool first = r < s0.n_pad;
+  const EvalThrSide& s = first ? s0 : s1;
+  if (!first) r -= s0.n_pad;
+  if (!s.hi || r >= s.n_pad) return;
+  unsigned m = 0u;
+  for (int k = 0; k < EVAL_EMAX_SHARDS; ++k) m = max(m, s.emax_other[k]);
+  const double E = score_error_bound((double)s.err[r], (double)__uint_as_float(m), d_pad, mode);
+  const double sgt = s.sgt[r];  // NaN (no GT, padding) or +inf (every GT NaN): never counted
+  s.hi[r] = sgt < INFINITY ? f32_round_up(sgt + E) : INFINITY;
+  s.lo[r] = sgt < INFINITY ? f32_round_down(sgt - E) : INFINITY;
+}
+
 extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode, const int64_t* row_off,
                                const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx, void* ws,
                                int64_t ws_bytes, int64_t cand_cap, int64_t* out, int32_t timing_slot) {
@@ -1515,7 +1555,7 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   SimArgs a = make_args(q, g, mode);
   // thresholds derived in the GEMM from the prep's GT scores and per-row bounds (row_hi / col_hi only
   // mark the directions that are on)
-  a.thr_gt = 1;
+  a.thr_gt = !sim_uses_phased(mode, q->n_pad, g->n_pad);
   a.q_err = mode_err(q, mode);
   a.g_err = mode_err(g, mode);
   a.q_emax = c.emax + (0 * 3 + mode_slot(mode)) * cmve::EMAX_SHARDS;
@@ -1539,6 +1579,15 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   a.tile_buckets = tile_buckets;
   a.nbn64 = (int)(g->n_pad >> 6);
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
+  if (!a.thr_gt) {
+    EvalThrSide t0{a.row_sgt, a.q_err, a.g_emax, row_off ? sq.thr_hi : nullptr, sq.thr_lo, q->n_pad};
+    EvalThrSide t1{a.col_sgt, a.g_err, a.q_emax, col_off ? sg.thr_hi : nullptr, sg.thr_lo, g->n_pad};
+    const int64_t nthr = q->n_pad + g->n_pad;
+    hipLaunchKernelGGL(eval_thr_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, t0, t1, q->d_pad,
+                       (int)mode);
+    st = check_launch("eval_thr_kernel");
+    if (st) return st;
+  }
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));

@@ -508,9 +508,10 @@ def test_bench_shape_ranks_against_independent_fp64(torch_cuda):
 
 
 @pytest.mark.parametrize("nq,ng,d", [(3, 129, 100), (130, 257, 64), (1000, 1000, 1024), (257, 300, 1536),
-                                     (2000, 600, 512), (64, 5000, 128)])
+                                     (2000, 600, 512), (64, 5000, 128), (4096, 8192, 64)])
 def test_rank_session_shapes_against_oracle(torch_cuda, nq, ng, d):
-    """cmve_eval_ranks on ragged shapes (G128 and G256 rank GEMMs), empty GT lists and multi-GT lists,
+    """cmve_eval_ranks on ragged shapes (G64 / G128 rank GEMMs with in-kernel thresholds; 4096 x 8192 = 512
+    tiles of 256^2 takes the persistent G256 kernel behind eval_thr_kernel), empty GT lists and multi-GT lists,
     fp32 and fp64 rows: ranks == the oracle's exact counts, R@K sums == the ranks'."""
     import torch
     from cmve import engine
