@@ -8,8 +8,8 @@
 //                          thresholds from the GT scores itself (SimArgs::thr_gt)
 //   3. eval_fix_kernel     K5b fp64 re-score of the undecided pairs, 4 waves per block, no tail
 //   4. eval_finish_kernel  a block per 256 rows: the 1-based ranks, R@1/5/10 + rank sums per direction
-//                          (block sums added into the stats head); block 0 also the sets' err_max (from
-//                          the prep's shards), the pair total and the overflow size
+//                          (block sums added into the stats head); two more blocks: the pair total and
+//                          overflow size, and the sets' err_max (from the prep's shards)
 // Round 2 first ran this as three launches whose LAST blocks derived the thresholds and the ranks
 // (an agent-scope arrival hand-off): per-block stamps put ~5-6 us on each arrival chain and 4-7 us on
 // each one-block tail, against ~1 us per kernel boundary; the boundaries replace them.
@@ -33,6 +33,18 @@ template <typename TA, typename TB>
 __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide& B, const EvalCommon& c, int64_t row,
                                               const TA* __restrict__ x, uint16_t* hrow, uint16_t* lrow,
                                               uint16_t* frow, int lane, float (&eb)[3]) {
+  // the first GT partner's row is loaded beside the row itself (its index is known up front): the
+  // GT score then needs no second HBM round trip after the pack
+  const int64_t g_beg = A.off ? A.off[row] : 0, g_end = A.off ? A.off[row + 1] : 0;
+  double w0[4][4];
+  if (g_beg < g_end) {
+    const TB* y = (const TB*)B.raw + (int64_t)A.idx[g_beg] * B.ld;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t k = (int64_t)lane * 4 + 256 * m;
+      if (k < c.d) load4d(y + k, w0[m]);
+    }
+  }
   double v[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -105,13 +117,20 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
   if (!A.off) return;
   double best = -INFINITY;
   bool any = false;
-  for (int64_t g = A.off[row]; g < A.off[row + 1]; ++g) {
-    const TB* y = (const TB*)B.raw + (int64_t)A.idx[g] * B.ld;
+  for (int64_t g = g_beg; g < g_end; ++g) {
     double w[4][4];
+    if (g == g_beg) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int64_t k = (int64_t)lane * 4 + 256 * m;
-      if (k < c.d) load4d(y + k, w[m]);
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[m][q] = w0[m][q];
+    } else {
+      const TB* y = (const TB*)B.raw + (int64_t)A.idx[g] * B.ld;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int64_t k = (int64_t)lane * 4 + 256 * m;
+        if (k < c.d) load4d(y + k, w[m]);
+      }
     }
     double dot = 0.0, yy = 0.0;
 #pragma unroll
@@ -130,7 +149,7 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
     }
   }
   if (lane == 0) {
-    A.sgt[row] = any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN);
+    A.sgt[row] = any ? best : (g_end > g_beg ? (double)INFINITY : (double)NAN);
     A.cnt[row] = 0;
   }
 }
@@ -277,7 +296,7 @@ __global__ __launch_bounds__(FIX_NT) void eval_fix_kernel(EvalSide q, EvalSide g
   EVAL_STAMP(c, 2, 1);
 }
 
-// the pair total / overflow size (cand_finalize_kernel's), block 0
+// the pair total / overflow size (cand_finalize_kernel's), one block
 __device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
   __shared__ unsigned long long redt[2 * FIN_NW], redm[2 * FIN_NW];
   unsigned long long tot[1] = {0}, mx[1] = {0};
@@ -296,7 +315,7 @@ __device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
 
 // err_max of both sides (all three planes, real rows, NaN skipped: err_max_kernel's result) as
 // cmve_pack_rows leaves it, folded from the prep's shards, which are zeroed for the next evaluation
-// (the rank GEMM has read them); block 0
+// (the rank GEMM has read them); one block
 __device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
   if (threadIdx.x < 6) {
     unsigned m = 0u;
@@ -315,9 +334,12 @@ __global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSid
   EVAL_STAMP(c, 1, 0);
   if (c.dbg & 32) return;
   __shared__ unsigned long long red[9 * FIN_NW];
-  if (blockIdx.x == 0) {
-    finish_buckets(c);
-    finish_err_max(q, g, c);
+  const unsigned nrank = gridDim.x - 2;  // the last two blocks: pair total / overflow, err_max
+  if (blockIdx.x >= nrank) {
+    if (blockIdx.x == nrank) finish_buckets(c);
+    else finish_err_max(q, g, c);
+    EVAL_STAMP(c, 1, 1);
+    return;
   }
   unsigned long long acc[8] = {};
   const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
@@ -360,8 +382,8 @@ static int launch_eval_typed(const EvalSide& q, const EvalSide& g, const EvalCom
     return check_launch("eval_fix_kernel");
   }
   const int64_t nmax = q.n > g.n ? q.n : g.n;
-  hipLaunchKernelGGL((eval_finish_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT)), dim3(FIN_NT), 0, s,
-                     q, g, c);
+  hipLaunchKernelGGL((eval_finish_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2), dim3(FIN_NT), 0,
+                     s, q, g, c);
   return check_launch("eval_finish_kernel");
 }
 

@@ -203,11 +203,14 @@ constexpr size_t stage_bytes() {
 
 // staging ring depth of the 2-stage (non-phased) loop: the G64 tiles of small problems keep NS - 1
 // K-tiles in flight (a 1k x 1k x 1024 GEMM is latency-bound: with 2 stages every one of its 16 K-tiles
-// exposed a full L2 / Infinity-Cache round trip, ~1.2 us each against ~0.1 us of MFMAs); the vmcnt
-// immediate (<= 63) caps it for split-bf16, whose stages carry twice the loads
+// exposed a full L2 / Infinity-Cache round trip, ~1.2 us each against ~0.1 us of MFMAs).  4 stages
+// (64 KiB of LDS) rather than 8: a G64 block is bound by its 2 waves ISSUING the LDS-DMA pieces
+// (8 per wave per K-tile, ~2.7 us for the first 7 K-tiles of an 8-deep ring in the stamps), so a deeper
+// ring gains nothing alone, while 64 KiB lets two evaluations' rank GEMMs share a CU (two HIP streams:
+// 31.0 -> 26.6 us per evaluation, tools/eval_pipe.py)
 template <int MODE, int BM, int BN, bool PHASED>
 constexpr int ring_stages() {
-  return (PHASED || BM != 64 || BN != 64) ? 2 : (MODE == CMVE_SIM_BF16X3 ? 4 : 8);
+  return (PHASED || BM != 64 || BN != 64) ? 2 : 4;
 }
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
@@ -841,10 +844,18 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
   const int nk0 = a.nk0;
   for (int t = 0; t < NS - 1 && t < nk0; ++t) stage(t, t);
+  // K14 thresholds: the GT score / bound loads are issued behind the first K-tiles' loads and the rule
+  // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
+  double sgt_raw = 0.0;
+  float e_raw = 0.f;
+  const bool thr_dir = tid < BM ? a.row_hi != nullptr : a.col_hi != nullptr;
   if constexpr (epi_thr(EPI)) {
-    if (a.thr_gt) {  // overlaps the first K-tiles' loads
-      reduce_err_max();
-      fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+    if (a.thr_gt) {
+      reduce_err_max();  // scalar loads: retired by the first barrier's lgkmcnt(0)
+      if (thr_dir) {
+        sgt_raw = tid < BM ? a.row_sgt[m0 + tid] : a.col_sgt[n0 + tid - BM];
+        e_raw = tid < BM ? a.q_err[m0 + tid] : a.g_err[n0 + tid - BM];
+      }
     }
   }
   CMVE_STAMP(1);
@@ -912,6 +923,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the threshold loads, if any are still out)
+  if constexpr (epi_thr(EPI)) {
+    if (a.thr_gt && thr_dir) thr_of(sgt_raw, e_raw, tid < BM ? gmax_v : qmax_v, thr_hi_v, thr_lo_v);
+  }
   CMVE_STAMP(2);
   } else {
   stage(0, 0);
