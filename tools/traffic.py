@@ -11,7 +11,10 @@ import os
 import shutil
 import sys
 
-KERNEL = "sim_kernel<2, 1>"  # cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK>
+# cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK, G256 phased> -- the 1k-A headline's G64 rank GEMM is another
+# instantiation of the same template and must not be mixed in
+def is_g256_rank(name):
+    return "sim_kernel" in name and ("<2, 1, 2, 4, 8, true>" in name or "ILi2ELi1ELi2ELi4ELi8ELb1E" in name)
 
 
 def rows(pattern):
@@ -34,12 +37,12 @@ def main(outdir, tag):
         vals = []
         for r in rows(os.path.join(outdir, sub, "**", "*counter_collection.csv")):
             name = r.get("Kernel_Name", "")
-            if "sim_kernel" in name and ("<2, 1" in name or "ILi2ELi1E" in name) and r.get("Counter_Name") == counter:
+            if is_g256_rank(name) and r.get("Counter_Name") == counter:
                 vals.append(float(r["Counter_Value"]))
         res[counter] = vals
     f = res["FETCH_SIZE"]
     w = res["WRITE_SIZE"]
-    out = {"kernel": "cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK>", "tag": tag,
+    out = {"kernel": "cmve::sim_kernel<CMVE_SIM_F16, EPI_RANK, G256 phased>", "tag": tag,
            "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
            "write_kib_per_launch": (sum(w) / len(w)) if w else None}
     if f and w:
@@ -49,7 +52,7 @@ def main(outdir, tag):
     mf = {}
     for r in rows(os.path.join(outdir, "mfma", "**", "*counter_collection.csv")):
         name = r.get("Kernel_Name", "")
-        if "sim_kernel" in name and ("<2, 1" in name or "ILi2ELi1E" in name):
+        if is_g256_rank(name):
             d = mf.setdefault(r["Dispatch_Id"], {"dur": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     if mf:
@@ -60,7 +63,7 @@ def main(outdir, tag):
     # per-launch durations of the same kernel in the trace pass: the bench's timed launches are the
     # last `steps` ones (the earlier ones are the workspace-sizing call and the warm-up steps)
     tr = [r for r in rows(os.path.join(outdir, "trace", "**", "*kernel_trace.csv"))
-          if "sim_kernel<2, 1" in r.get("Kernel_Name", "")]
+          if is_g256_rank(r.get("Kernel_Name", ""))]
     if tr:
         tr.sort(key=lambda r: int(r["Start_Timestamp"]))
         ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in tr]

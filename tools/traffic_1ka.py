@@ -1,5 +1,5 @@
-"""Reduce the rocprofv3 passes of tools/profile_1ka.sh to per-launch figures of the three K14
-evaluation launches (pack + GT scores, rank GEMM, fix-up + ranks) of the 1k-A headline.
+"""Reduce the rocprofv3 passes of tools/profile_1ka.sh to per-launch figures of the four K14
+evaluation launches (pack + GT scores, rank GEMM, fix-up, ranks + R@K) of the 1k-A headline.
 
 HBM bytes per dispatch = 2 * FETCH_SIZE(KiB) * 1024 + WRITE_SIZE(KiB) * 1024 (gfx950 FETCH_SIZE
 half-count on wide reads, MI355X_MICROARCH.md).  Writes profiles/<tag>_1ka_traffic.json (read by
@@ -22,11 +22,16 @@ def rows(pattern):
     return out
 
 
+ROLES = ("pack_gt_scores", "rank_gemm", "fixup", "ranks_recall")
+
+
 def role(name):
     if "eval_prep_kernel" in name:
-        return "pack_gt_thresholds"
+        return "pack_gt_scores"
     if "eval_fix_kernel" in name:
-        return "fixup_ranks"
+        return "fixup"
+    if "eval_finish_kernel" in name:
+        return "ranks_recall"
     if "sim_kernel<2, 1" in name:
         return "rank_gemm"
     return None
@@ -50,7 +55,7 @@ def main(outdir, tag):
         if k:
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
     kernels = {}
-    for k in ("pack_gt_thresholds", "rank_gemm", "fixup_ranks"):
+    for k in ROLES:
         f, w = per[k]["FETCH_SIZE"], per[k]["WRITE_SIZE"]
         e = {"launches_traced": len(dur[k]),
              "trace_avg_ms": (sum(dur[k]) / len(dur[k])) if dur[k] else None,
