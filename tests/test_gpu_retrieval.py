@@ -536,3 +536,31 @@ def test_rank_session_shapes_against_oracle(torch_cuda, nq, ng, d):
         h = sess.host.numpy()
         assert list(h[0:4]) == [int((r <= 1).sum()), int((r <= 5).sum()), int((r <= 10).sum()), int(r.sum())]
         assert list(h[4:8]) == [int((c <= 1).sum()), int((c <= 5).sum()), int((c <= 10).sum()), int(c.sum())]
+
+
+def test_rank_session_on_its_own_stream(torch_cuda):
+    """RankSession(stream=...) launches on its own stream (no current-stream switch per evaluation) and
+    writes into caller-provided out slots: same ranks and R@K heads as the default-stream session."""
+    import torch
+    from cmve import engine, _lib
+    rng = np.random.default_rng(11)
+    nq, ng, d = 300, 700, 256
+    gal = rng.standard_normal((ng, d))
+    qs = gal[rng.integers(0, ng, nq)] + 2.0 * rng.standard_normal((nq, d))
+    row_gts = [[int(x)] for x in rng.integers(0, ng, nq)]
+    q_t = torch.from_numpy(qs).cuda()
+    g_t = torch.from_numpy(gal).cuda()
+    ref = engine.RankSession(nq, ng, d, row_gts=row_gts, dtype=torch.float64)
+    r0, _ = ref.run(q_t, g_t)
+    st = torch.cuda.Stream()
+    sess = engine.RankSession(nq, ng, d, row_gts=row_gts, dtype=torch.float64, stream=st)
+    r1, _ = sess.run(q_t, g_t)
+    assert np.array_equal(r0, r1)
+    ring = torch.zeros((3, sess.out.numel()), dtype=torch.int64, device="cuda")
+    for j in range(3):
+        sess.enqueue(q_t, g_t, out=ring[j])
+    st.synchronize()
+    H = _lib.EVAL_OUT_HEAD
+    for j in range(3):
+        assert ring[j, :H].tolist() == ref.host[:H].tolist()
+        assert np.array_equal(ring[j, H:H + nq].cpu().numpy(), r0)
