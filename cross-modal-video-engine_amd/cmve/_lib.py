@@ -97,6 +97,10 @@ SIGNATURES = {
     "cmve_eval_workspace": (C.c_int, [_P(Rows), _P(Rows), _i64, _P(_i64)]),
     "cmve_eval_ranks": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i32]),
     "cmve_eval_timing": (C.c_int, [_vp, _i32, _P(_f32)]),
+    "cmve_eval_graph_create": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp,
+                                         _P(_vp)]),
+    "cmve_eval_graph_launch": (C.c_int, [_vp, _vp]),
+    "cmve_eval_graph_destroy": (C.c_int, [_vp]),
     "cmve_merge_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
@@ -135,7 +139,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -469,7 +469,8 @@ class RankSession:
         rs.desc.raw_ld = src.stride(0)
         return src
 
-    def enqueue(self, captions, videos, timing_slot: int = -1, out: Optional[torch.Tensor] = None):
+    def enqueue(self, captions, videos, timing_slot: int = -1, out: Optional[torch.Tensor] = None,
+                _bind_only: bool = False):
         """Enqueue one evaluation on the current stream (no synchronisation).  The inputs must stay
         alive and unmodified until it completes.  out: optional int64 device tensor of
         ``EVAL_OUT_HEAD + n_q + n_g`` words receiving this evaluation's head + ranks instead of
@@ -493,8 +494,27 @@ class RankSession:
             c = self.col if self.col is not None else (None, None)
             self._args = (C.byref(self.q.desc), C.byref(self.g.desc), self.mode, _ptr(r[0]), _ptr(r[1]), _ptr(c[0]),
                           _ptr(c[1]), _ptr(self.ws), self.ws.numel(), self.cap)
+        if _bind_only:
+            return
         h = self._h if self._h is not None else handle(self.device)
         check(lib.cmve_eval_ranks(h, *self._args, _ptr(out), int(timing_slot)), "cmve_eval_ranks")
+
+    def graph(self, captions, videos, out: Optional[torch.Tensor] = None) -> "EvalGraph":
+        """One evaluation of these inputs into `out` (default self.out) captured into a HIP graph on the
+        session's stream (cmve_eval_graph_create): ``launch()`` replays it with one host call, same results
+        bit for bit.  Every address is baked in: the inputs must be device tensors of the session dtype read
+        in place (refill them between launches), and `out` stays where it is."""
+        for x in (captions, videos):
+            if not (torch.is_tensor(x) and x.device == self.device and x.dtype == self.dtype):
+                raise ValueError("RankSession.graph: inputs must be device tensors of the session dtype")
+        self.enqueue(captions, videos, out=out, _bind_only=True)
+        if self._bound[0] is not captions or self._bound[1] is not videos:
+            raise ValueError("RankSession.graph: inputs must be readable in place (rows contiguous)")
+        out = self.out if out is None else out
+        h = self._h if self._h is not None else handle(self.device)
+        gh = C.c_void_p()
+        check(lib.cmve_eval_graph_create(h, *self._args, _ptr(out), C.byref(gh)), "cmve_eval_graph_create")
+        return EvalGraph(gh.value, h, (captions, videos, out, self))
 
     def timing(self, slot: int):
         """(pack+thresholds, rank GEMM, fix-up+ranks) milliseconds of the evaluation that used `slot`."""
@@ -521,6 +541,28 @@ class RankSession:
         t2v = h[o:o + nq].copy() if self.row is not None else None
         v2t = h[o + nq:o + nq + ng].copy() if self.col is not None else None
         return t2v, v2t
+
+
+class EvalGraph:
+    """A captured RankSession evaluation (cmve_eval_graph_*): ``launch()`` enqueues it on the session's
+    stream with one host call.  Keeps its inputs, output and session alive."""
+
+    def __init__(self, gh: int, h: int, keep):
+        self._g, self._h, self._keep = gh, h, keep
+
+    def launch(self):
+        check(lib.cmve_eval_graph_launch(self._h, self._g), "cmve_eval_graph_launch")
+
+    def close(self):
+        if self._g:
+            lib.cmve_eval_graph_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
 
 def rank_from_matrix(errors, gts, transposed: bool = False, device=None) -> np.ndarray:

@@ -1613,6 +1613,55 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   return CMVE_OK;
 }
 
+// The graph form: the four launches of one cmve_eval_ranks call captured once (their kernel arguments --
+// every pointer and size -- are baked in) and replayed with one hipGraphLaunch per evaluation: the host
+// side of an evaluation drops from four kernel launches to one graph launch.
+struct cmve_eval_graph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+extern "C" int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
+                                      const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
+                                      const int32_t* col_idx, void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out,
+                                      cmve_eval_graph_t* graph) {
+  CMVE_REQUIRE(h && graph, "cmve_eval_graph_create: NULL handle / output");
+  *graph = nullptr;
+  CMVE_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+  const int st = cmve_eval_ranks(h, q, g, mode, row_off, row_idx, col_off, col_idx, ws, ws_bytes, cand_cap, out, -1);
+  hipGraph_t gr = nullptr;
+  const hipError_t e = hipStreamEndCapture(h->stream, &gr);
+  if (st) {  // (the argument check failed inside the capture: nothing was enqueued)
+    if (gr) (void)hipGraphDestroy(gr);
+    return st;
+  }
+  CMVE_HIP(e);
+  auto* eg = new cmve_eval_graph;
+  eg->graph = gr;
+  const hipError_t ie = hipGraphInstantiate(&eg->exec, gr, nullptr, nullptr, 0);
+  if (ie != hipSuccess) {
+    (void)hipGraphDestroy(gr);
+    delete eg;
+    CMVE_HIP(ie);
+  }
+  *graph = eg;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_graph_launch(cmve_handle_t h, cmve_eval_graph_t graph) {
+  CMVE_REQUIRE(h && graph && graph->exec, "cmve_eval_graph_launch: NULL handle / graph");
+  CMVE_HIP(hipGraphLaunch(graph->exec, h->stream));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_graph_destroy(cmve_eval_graph_t graph) {
+  if (!graph) return CMVE_OK;
+  if (graph->exec) CMVE_HIP(hipGraphExecDestroy(graph->exec));
+  if (graph->graph) CMVE_HIP(hipGraphDestroy(graph->graph));
+  delete graph;
+  return CMVE_OK;
+}
+
 extern "C" int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3) {
   CMVE_REQUIRE(h && ms3 && slot >= 0 && slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_timing: bad argument");
   hipEvent_t* ev = h->eval_ev[slot];

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 10
+#define CMVE_ABI_VERSION 11
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -355,19 +355,19 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
  * (the reference's per-validation chain LINAS-engine/validate.py:61-74 / tester.py:133-139:
  * evaluation.cal_error (evaluation.py:17-21) then util/metrics.eval_q2m t2v and v2t (metrics.py:124-157)).
  *   launch 1: pack q and g from their raw rows (as cmve_pack_rows), exact fp64 GT scores of both
- *             directions (as cmve_gt_thresholds), zeroed counters; its last block derives err_max
- *             and the rank thresholds;
- *   launch 2: the fused rank GEMM (as cmve_rank_mfma);
- *   launch 3: the fp64 fix-up (as cmve_rank_fixup); its last block writes the ranks (as cmve_gt_ranks),
- *             R@K sums and the pair total.
+ *             directions (as cmve_gt_thresholds), zeroed counters, err_max shards;
+ *   launch 2: the fused rank GEMM (as cmve_rank_mfma), deriving the rank thresholds from the GT scores
+ *             and the err_max shards in-kernel (a G256-sized problem gets them from one more small launch);
+ *   launch 3: the fp64 fix-up (as cmve_rank_fixup);
+ *   launch 4: the ranks (as cmve_gt_ranks), R@K sums, the pair total and the sets' err_max.
  * The numbers equal the separate-launch path bit for bit.  q/g: packed sets (their planes, norms and
  * bounds are written; raw must point at the current rows).  row_off/row_idx: t2v GT lists of q's rows
  * into g (NULL: t2v off); col_off/col_idx: v2t GT lists of g's rows into q (NULL: v2t off).
- * ws: cmve_eval_workspace bytes, ZEROED ONCE when allocated (its arrival counters reset themselves).
+ * ws: cmve_eval_workspace bytes, ZEROED ONCE when allocated (its err_max shards reset themselves).
  * out (int64, 16 + q->n + g->n): out[0..4) t2v #rank<=1, #<=5, #<=10, sum of ranks; out[4..8) the same
  * for v2t; out[8] undecided pairs; out[9] 0, or the cand_cap a retry needs (a bucket overflowed: the
  * ranks are incomplete); out[16 ..] t2v ranks, then v2t ranks (1-based; cmve_gt_ranks' rules).
- * timing_slot in [0, CMVE_EVAL_TIMING_SLOTS) records handle events around the three launches
+ * timing_slot in [0, CMVE_EVAL_TIMING_SLOTS) records handle events around the launches
  * (cmve_eval_timing reads them); -1 records none.
  */
 #define CMVE_EVAL_TIMING_SLOTS 32
@@ -376,9 +376,22 @@ int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand
 int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
                     const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx,
                     void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out, int32_t timing_slot);
-/* Durations (ms) of the pack+threshold launch, the rank GEMM and the fix-up+ranks launch of the
+/* Durations (ms) of the pack launch, the rank GEMM and the fix-up + ranks launches of the
  * cmve_eval_ranks call that used `slot` (waits for its last event). */
 int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3);
+/* Graph form of cmve_eval_ranks for an evaluation repeated on fixed buffers (the reference re-runs
+ * validate.py:61-74 on new embeddings written into the same encode_* buffers; the bench's pipelined
+ * steps): create captures the launches of one cmve_eval_ranks call (same arguments, no timing) on h's
+ * stream into a HIP graph; every pointer and size is baked in, so q->raw / g->raw, the GT lists, ws and
+ * out must stay at their addresses.  launch replays it on h's stream with one host call (same results
+ * bit for bit); destroy frees it. */
+typedef struct cmve_eval_graph* cmve_eval_graph_t;
+int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
+                           const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
+                           const int32_t* col_idx, void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out,
+                           cmve_eval_graph_t* graph);
+int cmve_eval_graph_launch(cmve_handle_t h, cmve_eval_graph_t graph);
+int cmve_eval_graph_destroy(cmve_eval_graph_t graph);
 
 /*
  * C3 -- k-way merge of per-shard exact top-k lists (the gallery sharded over ranks, SURVEY.md 8e;

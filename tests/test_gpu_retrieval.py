@@ -564,3 +564,49 @@ def test_rank_session_on_its_own_stream(torch_cuda):
     for j in range(3):
         assert ring[j, :H].tolist() == ref.host[:H].tolist()
         assert np.array_equal(ring[j, H:H + nq].cpu().numpy(), r0)
+
+
+def test_rank_session_graph_replays(torch_cuda):
+    """cmve_eval_graph_*: a captured evaluation replayed many times (several graphs round-robin on one
+    stream, outputs in their own slots) gives the direct path's ranks and R@K heads every time, and reads
+    its inputs in place (refilled rows -> the new rows' ranks)."""
+    import torch
+    from cmve import engine, _lib
+    rng = np.random.default_rng(12)
+    nq, ng, d = 500, 900, 384
+    gal = rng.standard_normal((ng, d))
+    qs = gal[rng.integers(0, ng, nq)] + 2.0 * rng.standard_normal((nq, d))
+    row_gts = [[int(x)] for x in rng.integers(0, ng, nq)]
+    col_gts = [[int(x)] for x in rng.integers(0, nq, ng)]
+    q_t = torch.from_numpy(qs).cuda()
+    g_t = torch.from_numpy(gal).cuda()
+    ref = engine.RankSession(nq, ng, d, row_gts=row_gts, col_gts=col_gts, dtype=torch.float64)
+    r0, c0 = ref.run(q_t, g_t)
+    head0 = ref.host[:10].tolist()
+    st = torch.cuda.Stream()
+    sess = engine.RankSession(nq, ng, d, row_gts=row_gts, col_gts=col_gts, dtype=torch.float64, stream=st)
+    sess.run(q_t, g_t)
+    torch.cuda.synchronize()
+    ring = torch.zeros((4, sess.out.numel()), dtype=torch.int64, device="cuda")
+    graphs = [sess.graph(q_t, g_t, out=ring[j]) for j in range(4)]
+    H = _lib.EVAL_OUT_HEAD
+    for rep in range(12):
+        for j in range(4):
+            graphs[j].launch()
+        st.synchronize()
+        heads = ring[:, :10].cpu().tolist()
+        assert all(h == head0 for h in heads), (rep, heads)
+        assert np.array_equal(ring[rep % 4, H:H + nq].cpu().numpy(), r0)
+        assert np.array_equal(ring[rep % 4, H + nq:H + nq + ng].cpu().numpy(), c0)
+        ring.zero_()
+        torch.cuda.synchronize()
+    qs2 = gal[rng.integers(0, ng, nq)] + 2.0 * rng.standard_normal((nq, d))
+    q_t.copy_(torch.from_numpy(qs2))
+    torch.cuda.synchronize()
+    graphs[1].launch()
+    st.synchronize()
+    r2, c2 = ref.run(torch.from_numpy(qs2).cuda(), g_t)
+    assert np.array_equal(ring[1, H:H + nq].cpu().numpy(), r2)
+    assert np.array_equal(ring[1, H + nq:H + nq + ng].cpu().numpy(), c2)
+    for gr in graphs:
+        gr.close()

@@ -39,4 +39,8 @@ args = sess._args
 out_p = engine._ptr(sess.out)
 f = _lib.lib.cmve_eval_ranks
 t("raw_ctypes_call", lambda: f(h, *args, out_p, -1), 2000)
+gsess, gct, gvt, _ = bench.c1_session(dev, st)
+gsess.run(gct, gvt)
+gr = gsess.graph(gct, gvt)
+t("graph_launch", gr.launch, 2000)
 print(json.dumps({"host_us": res}))
