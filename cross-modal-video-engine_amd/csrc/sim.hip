@@ -139,42 +139,6 @@ __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
   return v;
 }
 
-// One row's 4 scores against its thresholds, hand-scheduled: count = #{s > hi} (exact v_cmp,
-// NaN never counts) and a lane mask of "some s in [lo, hi]" (v_med3 clamp == s).  The compiler
-// routes every compare through VCC and pads each with s_nop 1 before the reader; here the four
-// masks go to separate SGPR pairs and are read >= 3 instructions later (no wait states needed).
-__device__ __forceinline__ uint32_t row4_count_hit(float s0, float s1, float s2, float s3, float hi, float lo,
-                                                   unsigned long long& hit) {
-  uint32_t c;
-  float t0, t1, t2, t3;
-  unsigned long long m0, m1, m2, m3, h, cc;
-  asm("v_cmp_gt_f32_e64 %[m0], %[s0], %[hi]\n\t"
-      "v_cmp_gt_f32_e64 %[m1], %[s1], %[hi]\n\t"
-      "v_cmp_gt_f32_e64 %[m2], %[s2], %[hi]\n\t"
-      "v_cmp_gt_f32_e64 %[m3], %[s3], %[hi]\n\t"
-      "v_med3_f32 %[t0], %[s0], %[lo], %[hi]\n\t"
-      "v_med3_f32 %[t1], %[s1], %[lo], %[hi]\n\t"
-      "v_med3_f32 %[t2], %[s2], %[lo], %[hi]\n\t"
-      "v_med3_f32 %[t3], %[s3], %[lo], %[hi]\n\t"
-      "v_cndmask_b32_e64 %[c], 0, 1, %[m0]\n\t"
-      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m1]\n\t"
-      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m2]\n\t"
-      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m3]\n\t"
-      "v_cmp_eq_f32_e64 %[m0], %[t0], %[s0]\n\t"
-      "v_cmp_eq_f32_e64 %[m1], %[t1], %[s1]\n\t"
-      "v_cmp_eq_f32_e64 %[m2], %[t2], %[s2]\n\t"
-      "v_cmp_eq_f32_e64 %[m3], %[t3], %[s3]\n\t"
-      "s_nop 1\n\t"
-      "s_or_b64 %[h], %[m0], %[m1]\n\t"
-      "s_or_b64 %[h], %[h], %[m2]\n\t"
-      "s_or_b64 %[h], %[h], %[m3]"
-      : [c] "=&v"(c), [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [m0] "=&s"(m0),
-        [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [h] "=&s"(h), [cc] "=&s"(cc)
-      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [hi] "v"(hi), [lo] "v"(lo));
-  hit |= h;
-  return c;
-}
-
 template <int MODE>
 __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
   if constexpr (MODE == CMVE_SIM_F16)
@@ -513,10 +477,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         }
       };
       const bool do_row = a.row_hi != nullptr, do_col = a.col_hi != nullptr;
-      // fast scoring of an unpadded tile: per score an exact count compare (v_cmp + v_addc) and an
-      // "inside [lo, hi]" test (v_med3 + v_cmp) folded into a wave mask; the exact undecided bits
-      // are recomputed only for i-blocks where some lane hit.  The epilogue is VALU-issue-bound
-      // (4 cycles per wave64 instruction x 128 scores per lane): every instruction per score counts.
+      // scoring pass: per score an exact count compare (v_cmp + v_addc) and the exact "inside [lo, hi]"
+      // bit (rank epilogues), or a wave-mask band test with the bits recomputed only where some lane hit
+      // (top-k).  The epilogue is VALU-issue-bound (4 cycles per wave64 instruction x 128 scores per
+      // lane): every instruction per score counts.
       auto fast_block = [&](auto row_c, auto col_c) {
         constexpr bool DR = decltype(row_c)::value, DC = decltype(col_c)::value;
         uint32_t ccnt[TN] = {};
@@ -530,14 +494,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           }
           uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
           bool hit = false;
-          if constexpr (DR && !DC && TN == 4) {  // the bench / t2v shape: hand-scheduled per row
-            unsigned long long hm = 0ull;
-            c0 = row4_count_hit(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], hm);
-            c1 = row4_count_hit(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], hm);
-            c2 = row4_count_hit(acc[i][0][2], acc[i][1][2], acc[i][2][2], acc[i][3][2], rhi[2], rlo[2], hm);
-            c3 = row4_count_hit(acc[i][0][3], acc[i][1][3], acc[i][2][3], acc[i][3][3], rhi[3], rlo[3], hm);
-            hit = hm != 0ull;  // wave-uniform
-          } else
+          if constexpr (EPI == EPI_TOPK) {
+          // top-k emission (a band hit is rare, ~0.1% of scores): a wave-mask hit test, the exact bits
+          // recomputed only for i-blocks where some lane hit
   #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const f32x4_t sc = acc[i][j];
@@ -559,6 +518,34 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           }
           if constexpr (DR) row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
           und[i] = __builtin_amdgcn_ballot_w64(hit) ? und_bits(i, rhi, rlo, DR, DC) : 0u;
+          } else {
+          // rank counts: the exact count and the exact band bits of every score in one pass -- at the
+          // bench data's band rates ~94% of i-blocks hold an undecided pair, so a wave-mask hit test
+          // followed by recomputing the bits cost more than writing them directly (16,384 x 131,072 rank
+          // pass 3.92 -> 3.83 ms, tools/ab4.sh)
+          uint32_t u = 0u;
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const f32x4_t sc = acc[i][j];
+            if constexpr (DR) {
+              c0 += sc[0] > rhi[0];
+              c1 += sc[1] > rhi[1];
+              c2 += sc[2] > rhi[2];
+              c3 += sc[3] > rhi[3];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) u |= (sc[r] >= rlo[r] && sc[r] <= rhi[r]) ? (1u << (j * 4 + r)) : 0u;
+            }
+            if constexpr (DC) {
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                ccnt[j] += sc[r] > chi[j];
+                u |= (sc[r] >= clo[j] && sc[r] <= chi[j]) ? (1u << (16 + j * 4 + r)) : 0u;
+              }
+            }
+          }
+          if constexpr (DR) row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+          und[i] = u;
+          }
         }
         if constexpr (DC) {
   #pragma unroll
