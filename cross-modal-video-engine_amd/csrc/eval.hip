@@ -243,7 +243,10 @@ __device__ __forceinline__ void block_reduce_k(T (&v)[K], T* red /* LDS [K + 1][
   for (int k = 0; k < K; ++k) v[k] = out[k];
 }
 
-constexpr int PREP_NT = 256;  // 4 rows per block: a 1k-A evaluation's 2,048 rows fill every CU
+#ifndef CMVE_PREP_NT
+#define CMVE_PREP_NT 256
+#endif
+constexpr int PREP_NT = CMVE_PREP_NT;  // 4 rows per block: a 1k-A evaluation's 2,048 rows fill every CU
 constexpr int PREP_NW = PREP_NT / 64;
 
 template <typename TQ, typename TG>
