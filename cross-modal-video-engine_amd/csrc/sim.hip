@@ -139,6 +139,48 @@ __device__ __forceinline__ uint32_t row_sum16(uint32_t v) {
   return v;
 }
 
+// One row's 4 scores (columns j = 0..3 of lane row R) against its thresholds, hand-scheduled:
+// returns #{s > hi} (exact v_cmp; NaN never counts) and ORs the exact "lo <= s <= hi" bits into u at
+// bit 4j + R (s >= lo and not s > hi: lo <= hi, or both NaN / +inf, for every threshold pair).  Every
+// lane mask goes to its own SGPR pair and is read >= 4 instructions after it is written, so no wait
+// states are needed (the compiler routed each compare through VCC with an s_nop before the reader).
+template <int R>
+__device__ __forceinline__ uint32_t row4_count_bits(float s0, float s1, float s2, float s3, float hi, float lo,
+                                                    uint32_t& u) {
+  uint32_t c, b0, b1, b2, b3;
+  unsigned long long m0, m1, m2, m3, l0, l1, l2, l3, cc;
+  asm("v_cmp_gt_f32_e64 %[m0], %[s0], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m1], %[s1], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m2], %[s2], %[hi]\n\t"
+      "v_cmp_gt_f32_e64 %[m3], %[s3], %[hi]\n\t"
+      "v_cmp_ge_f32_e64 %[l0], %[s0], %[lo]\n\t"
+      "v_cmp_ge_f32_e64 %[l1], %[s1], %[lo]\n\t"
+      "v_cmp_ge_f32_e64 %[l2], %[s2], %[lo]\n\t"
+      "v_cmp_ge_f32_e64 %[l3], %[s3], %[lo]\n\t"
+      "v_cndmask_b32_e64 %[c], 0, 1, %[m0]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m1]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m2]\n\t"
+      "v_addc_co_u32_e64 %[c], %[cc], %[c], 0, %[m3]\n\t"
+      "s_andn2_b64 %[l0], %[l0], %[m0]\n\t"
+      "s_andn2_b64 %[l1], %[l1], %[m1]\n\t"
+      "s_andn2_b64 %[l2], %[l2], %[m2]\n\t"
+      "s_andn2_b64 %[l3], %[l3], %[m3]\n\t"
+      "v_cndmask_b32_e64 %[b0], 0, 1, %[l0]\n\t"
+      "v_cndmask_b32_e64 %[b1], 0, 1, %[l1]\n\t"
+      "v_cndmask_b32_e64 %[b2], 0, 1, %[l2]\n\t"
+      "v_cndmask_b32_e64 %[b3], 0, 1, %[l3]\n\t"
+      "v_lshl_or_b32 %[u], %[b0], %[sh0], %[u]\n\t"
+      "v_lshl_or_b32 %[u], %[b1], %[sh1], %[u]\n\t"
+      "v_lshl_or_b32 %[u], %[b2], %[sh2], %[u]\n\t"
+      "v_lshl_or_b32 %[u], %[b3], %[sh3], %[u]"
+      : [c] "=&v"(c), [b0] "=&v"(b0), [b1] "=&v"(b1), [b2] "=&v"(b2), [b3] "=&v"(b3), [u] "+v"(u),
+        [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [l0] "=&s"(l0), [l1] "=&s"(l1),
+        [l2] "=&s"(l2), [l3] "=&s"(l3), [cc] "=&s"(cc)
+      : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [hi] "v"(hi), [lo] "v"(lo), [sh0] "n"(R),
+        [sh1] "n"(4 + R), [sh2] "n"(8 + R), [sh3] "n"(12 + R));
+  return c;
+}
+
 template <int MODE>
 __device__ __forceinline__ f32x4_t mfma(s16x8_t a, s16x8_t b, f32x4_t c) {
   if constexpr (MODE == CMVE_SIM_F16)
@@ -524,6 +566,17 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           // followed by recomputing the bits cost more than writing them directly (16,384 x 131,072 rank
           // pass 3.92 -> 3.83 ms, tools/ab4.sh)
           uint32_t u = 0u;
+#ifndef CMVE_EPI_C
+          if constexpr (DR && !DC && TN == 4) {  // t2v (the bench / gallery shape): hand-scheduled per row
+            c0 = row4_count_bits<0>(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], u);
+            c1 = row4_count_bits<1>(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], u);
+            c2 = row4_count_bits<2>(acc[i][0][2], acc[i][1][2], acc[i][2][2], acc[i][3][2], rhi[2], rlo[2], u);
+            c3 = row4_count_bits<3>(acc[i][0][3], acc[i][1][3], acc[i][2][3], acc[i][3][3], rhi[3], rlo[3], u);
+            row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+            und[i] = u;
+            continue;
+          }
+#endif
   #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const f32x4_t sc = acc[i][j];
