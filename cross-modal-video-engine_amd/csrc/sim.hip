@@ -331,7 +331,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           lo = a.row_lo[mo + tid];
         }
       }
-    } else if (a.col_hi) {
+    } else if (tid < BM + BN && a.col_hi) {
       if (!PHASED && a.thr_gt) thr_of(a.col_sgt[no + tid - BM], a.g_err[no + tid - BM], qmax_v, hi, lo);
       else {
         hi = a.col_hi[no + tid - BM];
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   };
   if constexpr (EPI_COLS) fetch_cols(n0, colv);
   if constexpr (epi_thr(EPI)) {
-    static_assert(NT == BM + BN, "one threshold pair per thread");
+    static_assert(NT >= BM + BN, "one threshold pair per thread (threads past BM + BN hold none)");
     for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
     // K14 thresholds need the block's err_max reduction first: the 2-stage / ring loops do both after
     // issuing their first loads (below).  The persistent G256 kernel never derives them (cmve_eval_ranks
@@ -463,17 +463,19 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         }
     } else {
       // thresholds from LDS; a disabled direction holds NaN, which no comparison passes (not even s = +inf)
-      lds_thr[tid] = thr_hi_v;
-      lds_thr[NT + tid] = thr_lo_v;
+      if (tid < BM + BN) {
+        lds_thr[tid] = thr_hi_v;
+        lds_thr[BM + BN + tid] = thr_lo_v;
+      }
       CMVE_BAR_LDS();
       CMVE_STAMP(4);
       const float* l_rhi = lds_thr + (rbase - m0);
-      const float* l_rlo = lds_thr + NT + (rbase - m0);
+      const float* l_rlo = lds_thr + BM + BN + (rbase - m0);
       float chi[TN], clo[TN];
   #pragma unroll
       for (int j = 0; j < TN; ++j) {
         chi[j] = lds_thr[BM + (cbase - n0) + j * 16];
-        clo[j] = lds_thr[NT + BM + (cbase - n0) + j * 16];
+        clo[j] = lds_thr[BM + BN + BM + (cbase - n0) + j * 16];
       }
       // Branch-free scoring pass: per score only compares and bit packing.  Undecided pairs are
       // recorded as bits (per i: bit j*4+r = row-undecided, bit 16+j*4+r = column-undecided) and
@@ -888,7 +890,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
   double sgt_raw = 0.0;
   float e_raw = 0.f;
-  const bool thr_dir = tid < BM ? a.row_hi != nullptr : a.col_hi != nullptr;
+  const bool thr_dir = tid < BM ? a.row_hi != nullptr : (tid < BM + BN && a.col_hi != nullptr);
   if constexpr (epi_thr(EPI)) {
     if (a.thr_gt) {
       reduce_err_max();  // scalar loads: retired by the first barrier's lgkmcnt(0)
@@ -1109,10 +1111,17 @@ static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStrea
       if (force == 2562) return launch_geo<MODE, EPI, 2, 4, 8, false>(a, nq_pad, ng_pad, stream);  // 2-stage BK64
     return launch_geo<MODE, EPI, 2, 4, 8, true>(a, nq_pad, ng_pad, stream);
   }
-  // G64 (2 waves, 64 x 64 tiles) when the 128^2 grid would leave most CUs idle (a 1k x 1k problem: 64
-  // tiles of 128^2 vs 256 of 64^2); every output element sees the same MFMA sequence in every geometry
-  if (force != 128 && (nq_pad / 128) * (ng_pad / 128) < 128 && nq_pad % 64 == 0 && ng_pad % 64 == 0)
+  // G64 (4 waves of 16 x 64, 64 x 64 tiles) when the 128^2 grid would leave most CUs idle (a 1k x 1k
+  // problem: 64 tiles of 128^2 vs 256 of 64^2); every output element sees the same MFMA sequence in every
+  // geometry.  4 waves rather than 2 of 32 x 64: the rank epilogue's scoring runs on all 4 SIMDs (2.0 ->
+  // 1.2 us per tile in the K14 stamps); the main loop stays at ~6.3 us (the CU's L2 -> LDS fill of 256 KiB)
+  if (force != 128 && (nq_pad / 128) * (ng_pad / 128) < 128 && nq_pad % 64 == 0 && ng_pad % 64 == 0) {
+#ifndef CMVE_G64_2W
+    return launch_geo<MODE, EPI, 4, 1, 1, false>(a, nq_pad, ng_pad, stream);
+#else
     return launch_geo<MODE, EPI, 2, 1, 2, false>(a, nq_pad, ng_pad, stream);
+#endif
+  }
   return launch_geo<MODE, EPI, 2, 2, 4, false>(a, nq_pad, ng_pad, stream);
 }
 
