@@ -288,6 +288,9 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide
 }
 
 constexpr int FIX_NT = 256;
+#ifndef CMVE_FIX_BLOCKS
+#define CMVE_FIX_BLOCKS 1024
+#endif
 
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(FIX_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
@@ -381,7 +384,7 @@ static int launch_eval_typed(const EvalSide& q, const EvalSide& g, const EvalCom
   if (phase == 1) {
     // 1,024 blocks of 4 waves, every wave one or two of the few thousand undecided pairs of an evaluation
     // of this size, in one flat walk (the rank fix-up's grid is sized for millions of pairs)
-    hipLaunchKernelGGL((eval_fix_kernel<TQ, TG>), dim3(1024u), dim3(FIX_NT), 0, s, q, g, c);
+    hipLaunchKernelGGL((eval_fix_kernel<TQ, TG>), dim3((unsigned)CMVE_FIX_BLOCKS), dim3(FIX_NT), 0, s, q, g, c);
     return check_launch("eval_fix_kernel");
   }
   const int64_t nmax = q.n > g.n ? q.n : g.n;
