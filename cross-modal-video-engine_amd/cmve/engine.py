@@ -404,9 +404,9 @@ class RankSession:
     """Resident exact GT-rank evaluation of a fixed problem (the reference re-runs
     ``encode_* -> cal_error -> cal_perf`` on new embeddings of the same sets every validation,
     ``LINAS-engine/validate.py:61-74``): the packed planes of both sets, the GT lists, thresholds,
-    counts and the undecided-pair list are allocated once, and one evaluation is THREE launches on
-    the caller's current stream (``cmve_eval_ranks``, K14): pack both sets + exact GT scores +
-    thresholds, the fused rank GEMM, the fp64 fix-up + ranks + R@K sums.
+    counts and the undecided-pair list are allocated once, and one evaluation is FOUR launches on
+    the session's stream (``cmve_eval_ranks``, K14): pack both sets + exact GT scores, the fused rank
+    GEMM (thresholds derived in-kernel), the fp64 fix-up, ranks + R@K sums.
     ``run(captions, videos)`` returns (t2v ranks, v2t ranks) exactly as ``gt_rank_counts`` does.
     Device tensors of the session's dtype are read in place (no copy); anything else is copied into
     the session's own buffers first.  An undecided-pair overflow grows the list and redoes the run.
@@ -450,7 +450,7 @@ class RankSession:
 
     @property
     def ncand(self) -> int:
-        """Undecided pairs of the last evaluation (synchronises)."""
+        """Undecided pairs of the last evaluation written into ``self.out`` (synchronises)."""
         return int(self.out[8].item())
 
     def _bind(self, rs: RowSet, x):

@@ -359,7 +359,7 @@ def test_unpadded_fast_epilogue_each_direction(torch_cuda, dirs, nq, ng):
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_rank_session_replays_match(golden, torch_cuda, dtype):
-    """RankSession (resident buffers, cmve_eval_ranks: three launches per evaluation): C1 ranks equal
+    """RankSession (resident buffers, cmve_eval_ranks: four launches per evaluation): C1 ranks equal
     the golden ranks on every repeat with the inputs read in place, new embeddings give the ranks
     gt_rank_counts computes for them, the on-device R@K sums match the ranks, and an undecided-pair
     overflow grows the list without changing the result."""
