@@ -27,6 +27,7 @@ TOPK_MAX = 2048
 MAX_CHUNKS = 16
 EVAL_TIMING_SLOTS = 32
 EVAL_OUT_HEAD = 16
+DIST_UNIQUE_ID_BYTES = 128  # CMVE_DIST_UNIQUE_ID_BYTES
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD, PW_DOT = 0, 1, 2, 3, 4, 5
@@ -101,6 +102,11 @@ SIGNATURES = {
                                          _P(_vp)]),
     "cmve_eval_graph_launch": (C.c_int, [_vp, _vp]),
     "cmve_eval_graph_destroy": (C.c_int, [_vp]),
+    "cmve_dist_unique_id": (C.c_int, [_vp]),
+    "cmve_dist_init": (C.c_int, [_vp, _i32, _i32, _vp]),
+    "cmve_dist_allgather_q": (C.c_int, [_vp, _vp, _i64, _i64, _vp]),
+    "cmve_dist_reduce_rank": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "cmve_dist_destroy": (C.c_int, [_vp]),
     "cmve_merge_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
     "cmve_gt_positions_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
@@ -139,7 +145,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -166,6 +166,7 @@ int cmve_set_stream(cmve_handle_t h, void* hip_stream) {
 
 int cmve_destroy(cmve_handle_t h) {
   if (h) {
+    dist_release(h);
     if (h->scratch) (void)hipFree(h->scratch);
     for (hipEvent_t e : h->ev)
       if (e) (void)hipEventDestroy(e);

@@ -21,6 +21,9 @@ struct cmve_handle {
   // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // RCCL communicator of cmve_dist_init (dist.hip), nullptr without one
+  void* comm = nullptr;
+  int nranks = 1, rank = 0;
 };
 
 namespace cmve {
@@ -29,6 +32,8 @@ void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // make h->scratch at least `bytes` (synchronises the stream and reallocates only when it grows)
 int ensure_scratch(cmve_handle* h, size_t bytes);
+// destroy the handle's RCCL communicator, if any (dist.hip)
+void dist_release(cmve_handle* h);
 
 #define CMVE_REQUIRE(cond, ...)            \
   do {                                     \

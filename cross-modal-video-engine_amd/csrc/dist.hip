@@ -1,0 +1,121 @@
+// Gallery-shard collectives of SURVEY.md 8(e) in the C ABI (8(b): cmve_dist_init / allgather_q /
+// reduce_rank; merge_topk is merge.hip), for a host that shards the gallery without torch.distributed.
+// Per batch (the reference never shards -- LINAS-engine/evaluation.py:17-21 scores one in-memory
+// gallery): all-gather the query rows over xGMI, every rank scores its resident shard, then one
+// all-reduce MAX of the per-shard best-GT scores (NaN -> -inf for "no GT in this shard") and one
+// all-reduce SUM of the better-than-GT counts.  RCCL is opened at cmve_dist_init with dlopen (no link
+// dependency: libcmve.so loads without it, and inside a torch process the RCCL torch already mapped
+// is reused, one RCCL per process).  Every collective is enqueued on the handle's stream.
+#include <dlfcn.h>
+#include <string.h>
+#include <rccl/rccl.h>
+
+#include "cmve_internal.h"
+
+namespace cmve {
+
+struct RcclApi {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*);
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*comm_destroy)(ncclComm_t);
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  const char* (*error_string)(ncclResult_t);
+};
+
+static const RcclApi* rccl_api() {
+  static RcclApi api{};
+  static int state = 0;  // 0 untried, 1 loaded, -1 unavailable
+  if (state) return state > 0 ? &api : nullptr;
+  void* lib = nullptr;
+  for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+    if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+  if (lib) {
+    api.get_unique_id = (decltype(api.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+    api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+    api.comm_destroy = (decltype(api.comm_destroy))dlsym(lib, "ncclCommDestroy");
+    api.all_gather = (decltype(api.all_gather))dlsym(lib, "ncclAllGather");
+    api.all_reduce = (decltype(api.all_reduce))dlsym(lib, "ncclAllReduce");
+    api.error_string = (decltype(api.error_string))dlsym(lib, "ncclGetErrorString");
+  }
+  const bool ok = lib && api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather &&
+                  api.all_reduce && api.error_string;
+  state = ok ? 1 : -1;
+  return ok ? &api : nullptr;
+}
+
+#define CMVE_RCCL(api, call, what)                                                         \
+  do {                                                                                     \
+    const ncclResult_t r_ = (call);                                                        \
+    if (r_ != ncclSuccess) {                                                               \
+      ::cmve::set_error("%s: RCCL error %d: %s", what, (int)r_, (api)->error_string(r_));   \
+      return CMVE_E_HIP;                                                                   \
+    }                                                                                      \
+  } while (0)
+
+void dist_release(cmve_handle* h) {
+  if (!h->comm) return;  // (no dlopen for handles that never held a communicator)
+  const RcclApi* api = rccl_api();
+  if (api) (void)api->comm_destroy((ncclComm_t)h->comm);
+  h->comm = nullptr;
+}
+
+}  // namespace cmve
+
+using namespace cmve;
+
+extern "C" int cmve_dist_unique_id(void* id) {
+  CMVE_REQUIRE(id, "cmve_dist_unique_id: NULL output");
+  const RcclApi* api = rccl_api();
+  CMVE_REQUIRE(api, "cmve_dist_unique_id: RCCL (librccl.so) could not be opened");
+  ncclUniqueId u;
+  CMVE_RCCL(api, api->get_unique_id(&u), "cmve_dist_unique_id");
+  memcpy(id, &u, sizeof(u));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_init(cmve_handle_t h, int32_t nranks, int32_t rank, const void* id) {
+  CMVE_REQUIRE(h && id, "cmve_dist_init: NULL handle / id");
+  CMVE_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "cmve_dist_init: rank %d of %d", rank, nranks);
+  CMVE_REQUIRE(!h->comm, "cmve_dist_init: the handle already holds a communicator");
+  const RcclApi* api = rccl_api();
+  CMVE_REQUIRE(api, "cmve_dist_init: RCCL (librccl.so) could not be opened");
+  CMVE_HIP(hipSetDevice(h->device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t comm = nullptr;
+  CMVE_RCCL(api, api->comm_init_rank(&comm, nranks, u, rank), "cmve_dist_init");
+  h->comm = comm;
+  h->nranks = nranks;
+  h->rank = rank;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_allgather_q(cmve_handle_t h, const float* local, int64_t n_local, int64_t d,
+                                     float* gathered) {
+  CMVE_REQUIRE(h && h->comm, "cmve_dist_allgather_q: handle has no communicator (cmve_dist_init)");
+  CMVE_REQUIRE(n_local >= 0 && d > 0 && (n_local == 0 || (local && gathered)), "cmve_dist_allgather_q: bad argument");
+  const RcclApi* api = rccl_api();
+  CMVE_RCCL(api, api->all_gather(local, gathered, (size_t)(n_local * d), ncclFloat32, (ncclComm_t)h->comm, h->stream),
+            "cmve_dist_allgather_q");
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_reduce_rank(cmve_handle_t h, double* best_gt, int32_t* counts, int64_t n) {
+  CMVE_REQUIRE(h && h->comm, "cmve_dist_reduce_rank: handle has no communicator (cmve_dist_init)");
+  CMVE_REQUIRE(n >= 0 && (n == 0 || best_gt || counts), "cmve_dist_reduce_rank: bad argument");
+  const RcclApi* api = rccl_api();
+  if (best_gt)
+    CMVE_RCCL(api, api->all_reduce(best_gt, best_gt, (size_t)n, ncclFloat64, ncclMax, (ncclComm_t)h->comm, h->stream),
+              "cmve_dist_reduce_rank (max)");
+  if (counts)
+    CMVE_RCCL(api, api->all_reduce(counts, counts, (size_t)n, ncclInt32, ncclSum, (ncclComm_t)h->comm, h->stream),
+              "cmve_dist_reduce_rank (sum)");
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_destroy(cmve_handle_t h) {
+  CMVE_REQUIRE(h, "cmve_dist_destroy: NULL handle");
+  dist_release(h);
+  return CMVE_OK;
+}

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 11
+#define CMVE_ABI_VERSION 12
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -392,6 +392,27 @@ int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int3
                            cmve_eval_graph_t* graph);
 int cmve_eval_graph_launch(cmve_handle_t h, cmve_eval_graph_t graph);
 int cmve_eval_graph_destroy(cmve_eval_graph_t graph);
+
+/*
+ * Gallery-shard collectives over RCCL, for a host that shards the gallery
+ * without torch.distributed (the Python mirror's cmve/dist.py runs the same exchange through
+ * torch.distributed): every rank holds a resident shard; per batch the query rows are all-gathered,
+ * each rank scores its shard (cmve_gt_thresholds / cmve_rank_count / cmve_topk), then the best-GT
+ * scores are all-reduced MAX (NaN -> -inf marks "no GT in this shard") and the better-than-GT counts
+ * SUM; top-k lists merge with cmve_merge_topk.  The reference never shards (LINAS-engine/evaluation.py:17-21
+ * and inference.py:78-79 score one in-memory gallery); these replace nothing one-for-one.
+ * RCCL (librccl.so) is opened with dlopen at first use.  cmve_dist_unique_id fills 128 bytes on ONE rank;
+ * the host distributes them; cmve_dist_init binds a communicator of `nranks` to the handle (its device,
+ * its stream for every collective); cmve_destroy releases it.
+ * allgather_q: gathered[r * n_local + i] = rank r's local row i (n_local rows of d fp32 per rank).
+ * reduce_rank: best_gt (fp64, in place, MAX) and / or counts (int32, in place, SUM), n entries each.
+ */
+#define CMVE_DIST_UNIQUE_ID_BYTES 128
+int cmve_dist_unique_id(void* id);
+int cmve_dist_init(cmve_handle_t h, int32_t nranks, int32_t rank, const void* id);
+int cmve_dist_allgather_q(cmve_handle_t h, const float* local, int64_t n_local, int64_t d, float* gathered);
+int cmve_dist_reduce_rank(cmve_handle_t h, double* best_gt, int32_t* counts, int64_t n);
+int cmve_dist_destroy(cmve_handle_t h);
 
 /*
  * C3 -- k-way merge of per-shard exact top-k lists (the gallery sharded over ranks, SURVEY.md 8e;
