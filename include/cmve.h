@@ -403,7 +403,8 @@ int cmve_eval_graph_destroy(cmve_eval_graph_t graph);
  * and inference.py:78-79 score one in-memory gallery); these replace nothing one-for-one.
  * RCCL (librccl.so) is opened with dlopen at first use.  cmve_dist_unique_id fills 128 bytes on ONE rank;
  * the host distributes them; cmve_dist_init binds a communicator of `nranks` to the handle (its device,
- * its stream for every collective); cmve_destroy releases it.
+ * its stream for every collective; it makes the handle's device the calling thread's current device);
+ * cmve_destroy releases it.
  * allgather_q: gathered[r * n_local + i] = rank r's local row i (n_local rows of d fp32 per rank).
  * reduce_rank: best_gt (fp64, in place, MAX) and / or counts (int32, in place, SUM), n entries each.
  */
