@@ -28,7 +28,9 @@ static const RcclApi* rccl_api() {
   static int state = 0;  // 0 untried, 1 loaded, -1 unavailable
   if (state) return state > 0 ? &api : nullptr;
   void* lib = nullptr;
-  for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+  // the soname first: a process that already mapped an RCCL (torch's, soname librccl.so.1) gets THAT one
+  // back instead of a second copy from the library path
+  for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
     if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
   if (lib) {
     api.get_unique_id = (decltype(api.get_unique_id))dlsym(lib, "ncclGetUniqueId");
