@@ -323,14 +323,18 @@ __device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
 // cmve_pack_rows leaves it, folded from the prep's shards, which are zeroed for the next evaluation
 // (the rank GEMM has read them); one block
 __device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
-  if (threadIdx.x < 6) {
-    unsigned m = 0u;
-    for (int k = 0; k < EMAX_SHARDS; ++k) m = max(m, c.emax[threadIdx.x * EMAX_SHARDS + k]);
-    const float* e = threadIdx.x < 3 ? q.err_max : g.err_max;
-    ((float*)e)[threadIdx.x % 3] = __uint_as_float(m);
+  // one wave per (side, plane): each lane reads one of its 64 shards (one round of loads, not 64 serial
+  // ones), a wave max, and zeroes the word it read
+  static_assert(EMAX_SHARDS == 64, "one shard per lane");
+  const int lane = threadIdx.x & 63;
+  for (int sp = threadIdx.x >> 6; sp < 6; sp += FIN_NW) {
+    unsigned* w = &c.emax[sp * EMAX_SHARDS + lane];
+    unsigned m = *w;
+    *w = 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+    if (lane == 0) ((float*)(sp < 3 ? q.err_max : g.err_max))[sp % 3] = __uint_as_float(m);
   }
-  __syncthreads();  // every fold has read the shards
-  for (int k = threadIdx.x; k < 6 * EMAX_SHARDS; k += FIN_NT) c.emax[k] = 0u;
 }
 
 // The ranks of both directions (cmve_gt_ranks' rules) for this block's 256 rows of each side and, per
