@@ -106,6 +106,7 @@ SIGNATURES = {
     "cmve_dist_init": (C.c_int, [_vp, _i32, _i32, _vp]),
     "cmve_dist_allgather_q": (C.c_int, [_vp, _vp, _i64, _i64, _vp]),
     "cmve_dist_reduce_rank": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "cmve_dist_allgather_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
     "cmve_dist_destroy": (C.c_int, [_vp]),
     "cmve_merge_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
@@ -145,7 +146,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -8,6 +8,7 @@
 #include "cmve_internal.h"
 #include <stdarg.h>
 #include <stdio.h>
+#include <atomic>
 
 namespace cmve {
 
@@ -29,6 +30,20 @@ int check_launch(const char* what) {
     return CMVE_E_HIP;
   }
   return CMVE_OK;
+}
+
+int device_cus() {
+  // one slot per device ordinal: a host thread per GPU may ask concurrently (relaxed atomics: the value
+  // is a pure function of the device, so a racing double query stores the same number)
+  static std::atomic<int> cus[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int c = cus[dev].load(std::memory_order_relaxed);
+  if (!c) {
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    cus[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
 }
 
 // ---------------------------------------------------------------------------

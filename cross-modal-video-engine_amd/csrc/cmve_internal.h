@@ -34,6 +34,11 @@ int check_launch(const char* what);
 int ensure_scratch(cmve_handle* h, size_t bytes);
 // destroy the handle's RCCL communicator, if any (dist.hip)
 void dist_release(cmve_handle* h);
+// k-way merge of sorted top-k runs (merge.hip): entry (q, run l, pos p) at q * q_stride + l * l_stride + p
+int merge_topk_launch(hipStream_t s, const int64_t* ids, const double* scores, int64_t n_q, int lists, int k_in,
+                      int64_t q_stride, int64_t l_stride, int k_out, int64_t* out_ids, double* out_scores);
+// compute units of the current device (queried once per device; thread-safe)
+int device_cus();
 
 #define CMVE_REQUIRE(cond, ...)            \
   do {                                     \

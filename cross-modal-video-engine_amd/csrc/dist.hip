@@ -1,9 +1,10 @@
 // Gallery-shard collectives of SURVEY.md 8(e) in the C ABI (8(b): cmve_dist_init / allgather_q /
-// reduce_rank; merge_topk is merge.hip), for a host that shards the gallery without torch.distributed.
+// reduce_rank / allgather_topk), for a host that shards the gallery without torch.distributed (the
+// Python host mirror, cmve/dist.py, runs the same exchange over torch.distributed).
 // Per batch (the reference never shards -- LINAS-engine/evaluation.py:17-21 scores one in-memory
 // gallery): all-gather the query rows over xGMI, every rank scores its resident shard, then one
-// all-reduce MAX of the per-shard best-GT scores (NaN -> -inf for "no GT in this shard") and one
-// all-reduce SUM of the better-than-GT counts.  RCCL is opened at cmve_dist_init with dlopen (no link
+// all-reduce MAX of the per-shard best-GT scores and one all-reduce SUM of the better-than-GT counts;
+// top-k runs are all-gathered and merged on the device.  RCCL is opened with dlopen at first use (no link
 // dependency: libcmve.so loads without it, and inside a torch process the RCCL torch already mapped
 // is reused, one RCCL per process).  Every collective is enqueued on the handle's stream.
 #include <dlfcn.h>
@@ -21,29 +22,31 @@ struct RcclApi {
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
   const char* (*error_string)(ncclResult_t);
+  bool ok = false;
 };
 
-static const RcclApi* rccl_api() {
-  static RcclApi api{};
-  static int state = 0;  // 0 untried, 1 loaded, -1 unavailable
-  if (state) return state > 0 ? &api : nullptr;
+static RcclApi load_rccl() {
+  RcclApi api{};
   void* lib = nullptr;
   // the soname first: a process that already mapped an RCCL (torch's, soname librccl.so.1) gets THAT one
   // back instead of a second copy from the library path
   for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
     if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
-  if (lib) {
-    api.get_unique_id = (decltype(api.get_unique_id))dlsym(lib, "ncclGetUniqueId");
-    api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(lib, "ncclCommInitRank");
-    api.comm_destroy = (decltype(api.comm_destroy))dlsym(lib, "ncclCommDestroy");
-    api.all_gather = (decltype(api.all_gather))dlsym(lib, "ncclAllGather");
-    api.all_reduce = (decltype(api.all_reduce))dlsym(lib, "ncclAllReduce");
-    api.error_string = (decltype(api.error_string))dlsym(lib, "ncclGetErrorString");
-  }
-  const bool ok = lib && api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather &&
-                  api.all_reduce && api.error_string;
-  state = ok ? 1 : -1;
-  return ok ? &api : nullptr;
+  if (!lib) return api;
+  api.get_unique_id = (decltype(api.get_unique_id))dlsym(lib, "ncclGetUniqueId");
+  api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(lib, "ncclCommInitRank");
+  api.comm_destroy = (decltype(api.comm_destroy))dlsym(lib, "ncclCommDestroy");
+  api.all_gather = (decltype(api.all_gather))dlsym(lib, "ncclAllGather");
+  api.all_reduce = (decltype(api.all_reduce))dlsym(lib, "ncclAllReduce");
+  api.error_string = (decltype(api.error_string))dlsym(lib, "ncclGetErrorString");
+  api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather && api.all_reduce &&
+           api.error_string;
+  return api;
+}
+
+static const RcclApi* rccl_api() {
+  static const RcclApi api = load_rccl();  // C++11 function-local static: initialised once, thread-safe
+  return api.ok ? &api : nullptr;
 }
 
 #define CMVE_RCCL(api, call, what)                                                         \
@@ -60,6 +63,30 @@ void dist_release(cmve_handle* h) {
   const RcclApi* api = rccl_api();
   if (api) (void)api->comm_destroy((ncclComm_t)h->comm);
   h->comm = nullptr;
+}
+
+// Best-GT score keys for the MAX all-reduce (cmve_gt_thresholds' per-shard encoding: NaN = no GT in
+// this shard, +inf = GTs here but every one scores NaN, else the best finite score).  Encoded, a finite
+// score beats "all NaN" (-1e300), which beats "no GT" (-inf); RCCL's MAX never sees a NaN.
+constexpr double NAN_GT_KEY = -1e300;
+
+__global__ __launch_bounds__(256) void gt_key_kernel(double* __restrict__ s, int64_t n, int decode) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double v = s[i];
+  if (!decode) {
+    if (v != v) s[i] = -INFINITY;
+    else if (v == INFINITY) s[i] = NAN_GT_KEY;
+  } else {
+    if (v == -INFINITY) s[i] = (double)NAN;
+    else if (v == NAN_GT_KEY) s[i] = INFINITY;
+  }
+}
+
+static int gt_keys(hipStream_t s, double* v, int64_t n, int decode) {
+  if (n == 0) return CMVE_OK;
+  hipLaunchKernelGGL(gt_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, v, n, decode);
+  return check_launch("gt_key_kernel");
 }
 
 }  // namespace cmve
@@ -107,13 +134,37 @@ extern "C" int cmve_dist_reduce_rank(cmve_handle_t h, double* best_gt, int32_t* 
   CMVE_REQUIRE(h && h->comm, "cmve_dist_reduce_rank: handle has no communicator (cmve_dist_init)");
   CMVE_REQUIRE(n >= 0 && (n == 0 || best_gt || counts), "cmve_dist_reduce_rank: bad argument");
   const RcclApi* api = rccl_api();
-  if (best_gt)
+  if (best_gt) {  // encode -> MAX -> decode, all on the handle's stream
+    int st = gt_keys(h->stream, best_gt, n, 0);
+    if (st) return st;
     CMVE_RCCL(api, api->all_reduce(best_gt, best_gt, (size_t)n, ncclFloat64, ncclMax, (ncclComm_t)h->comm, h->stream),
               "cmve_dist_reduce_rank (max)");
+    st = gt_keys(h->stream, best_gt, n, 1);
+    if (st) return st;
+  }
   if (counts)
     CMVE_RCCL(api, api->all_reduce(counts, counts, (size_t)n, ncclInt32, ncclSum, (ncclComm_t)h->comm, h->stream),
               "cmve_dist_reduce_rank (sum)");
   return CMVE_OK;
+}
+
+extern "C" int cmve_dist_allgather_topk(cmve_handle_t h, const int64_t* ids, const double* scores, int64_t n_q,
+                                        int32_t k, int64_t* gathered_ids, double* gathered_scores, int32_t k_out,
+                                        int64_t* out_ids, double* out_scores) {
+  CMVE_REQUIRE(h && h->comm, "cmve_dist_allgather_topk: handle has no communicator (cmve_dist_init)");
+  CMVE_REQUIRE(n_q >= 0 && k >= 1 && k_out >= 1 && h->nranks <= 64, "cmve_dist_allgather_topk: bad argument");
+  if (n_q == 0) return CMVE_OK;
+  CMVE_REQUIRE(ids && scores && gathered_ids && gathered_scores && out_ids && out_scores,
+               "cmve_dist_allgather_topk: NULL argument");
+  const RcclApi* api = rccl_api();
+  const size_t cnt = (size_t)(n_q * k);
+  CMVE_RCCL(api, api->all_gather(ids, gathered_ids, cnt, ncclInt64, (ncclComm_t)h->comm, h->stream),
+            "cmve_dist_allgather_topk (ids)");
+  CMVE_RCCL(api, api->all_gather(scores, gathered_scores, cnt, ncclFloat64, (ncclComm_t)h->comm, h->stream),
+            "cmve_dist_allgather_topk (scores)");
+  // rank-major [nranks][n_q][k]: query q's run from rank r starts at r * n_q * k + q * k
+  return merge_topk_launch(h->stream, gathered_ids, gathered_scores, n_q, h->nranks, k, k, (int64_t)n_q * k, k_out,
+                           out_ids, out_scores);
 }
 
 extern "C" int cmve_dist_destroy(cmve_handle_t h) {

@@ -21,22 +21,26 @@ __device__ __forceinline__ bool head_better(double sa, int64_t ia, double sb, in
   return ia < ib;
 }
 
+// entry (query q, run l, position p) at q * q_stride + l * l_stride + p: query-major runs side by side
+// (q_stride = lists * k_in, l_stride = k_in) or the rank-major layout of an all-gather (q_stride = k_in,
+// l_stride = n_q * k_in)
 __global__ __launch_bounds__(256) void merge_topk_kernel(const int64_t* __restrict__ ids,
                                                          const double* __restrict__ scores, int64_t n_q, int lists,
-                                                         int k_in, int k_out, int64_t* __restrict__ out_ids,
+                                                         int k_in, int64_t q_stride, int64_t l_stride, int k_out,
+                                                         int64_t* __restrict__ out_ids,
                                                          double* __restrict__ out_scores) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= n_q) return;
-  const int64_t row = q * (int64_t)lists * k_in;
+  const int64_t run = q * q_stride + (int64_t)lane * l_stride;
   int pos = 0;
   int64_t hid = -1;
   double hs = 0.0;
   auto load_head = [&]() {
     hid = -1;
     if (lane < lists && pos < k_in) {
-      hid = ids[row + (int64_t)lane * k_in + pos];
-      hs = scores[row + (int64_t)lane * k_in + pos];
+      hid = ids[run + pos];
+      hs = scores[run + pos];
     }
   };
   load_head();
@@ -67,6 +71,14 @@ __global__ __launch_bounds__(256) void merge_topk_kernel(const int64_t* __restri
   }
 }
 
+int merge_topk_launch(hipStream_t s, const int64_t* ids, const double* scores, int64_t n_q, int lists, int k_in,
+                      int64_t q_stride, int64_t l_stride, int k_out, int64_t* out_ids, double* out_scores) {
+  if (n_q == 0) return CMVE_OK;
+  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)((n_q + 3) / 4)), dim3(256), 0, s, ids, scores, n_q, lists,
+                     k_in, q_stride, l_stride, k_out, out_ids, out_scores);
+  return check_launch("merge_topk_kernel");
+}
+
 }  // namespace cmve
 
 using namespace cmve;
@@ -76,8 +88,6 @@ extern "C" int cmve_merge_topk(cmve_handle_t h, const int64_t* ids, const double
   CMVE_REQUIRE(h && ids && scores && out_ids && out_scores, "cmve_merge_topk: NULL argument");
   CMVE_REQUIRE(n_q >= 0 && lists >= 1 && lists <= 64 && k_in >= 1 && k_out >= 1,
                "cmve_merge_topk: need 1 <= lists <= 64, k_in >= 1, k_out >= 1");
-  if (n_q == 0) return CMVE_OK;
-  hipLaunchKernelGGL(merge_topk_kernel, dim3((unsigned)((n_q + 3) / 4)), dim3(256), 0, h->stream, ids, scores, n_q,
-                     (int)lists, (int)k_in, (int)k_out, out_ids, out_scores);
-  return check_launch("merge_topk_kernel");
+  return merge_topk_launch(h->stream, ids, scores, n_q, (int)lists, (int)k_in, (int64_t)lists * k_in, k_in, (int)k_out,
+                           out_ids, out_scores);
 }

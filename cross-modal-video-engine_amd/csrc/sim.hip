@@ -1057,12 +1057,10 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
   using G = Geo<WM, WN, TM>;
   const size_t lds = ring_stages<MODE, G::BM, G::BN, PHASED>() *
                      stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
-  static bool attr_done = false;
-  if (!attr_done) {
-    CMVE_HIP(hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr_done = true;
-  }
+  // once per instantiation; function-local static init is thread-safe (one host thread per shard / GPU)
+  static const hipError_t attr_err = hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  CMVE_HIP(attr_err);
   a.nblk_m = (int)(nq_pad / G::BM);
   a.nblk_n = (int)(ng_pad / G::BN);
   static const int gn_env = [] {
@@ -1072,13 +1070,7 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
   a.gn = gn_env > 0 ? gn_env : 8;
   unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
   if constexpr (PHASED) {  // persistent: one block per CU (a multiple of 8: the XCD map is blockIdx & 7)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      CMVE_HIP(hipGetDevice(&dev));
-      CMVE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-      cus = std::max(8, cus / 8 * 8);
-    }
+    const int cus = std::max(8, device_cus() / 8 * 8);
     nblocks = std::min<unsigned>(nblocks, (unsigned)cus);
   }
   hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, PHASED>), dim3(nblocks), dim3(G::NT), lds, stream, a);

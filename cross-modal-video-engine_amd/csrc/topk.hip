@@ -432,23 +432,15 @@ static int launch_gemv(const cmve_rows_t* q, const cmve_rows_t* g, float* ws, hi
   const uint16_t* gh = MODE == CMVE_SIM_F16 ? g->h16 : g->hi;
   const int nqt = q->n <= 16 ? 1 : 2;
   const size_t lds = (size_t)nqt * PL * 16 * g->d_pad * 2;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    CMVE_HIP(hipGetDevice(&dev));
-    CMVE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  const int cus = device_cus();
   const int64_t groups = (g->n + 15) / 16;
   // enough blocks for ~16 waves per CU, never more than one 16-row group per wave
   const unsigned nblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((groups + 3) / 4, (int64_t)cus * 4));
 #define GV(NQT)                                                                                                     \
   do {                                                                                                              \
-    static bool attr = false;                                                                                       \
-    if (!attr) {                                                                                                    \
-      CMVE_HIP(hipFuncSetAttribute((const void*)gemv_scores_kernel<MODE, NQT>,                                      \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                        \
-      attr = true;                                                                                                  \
-    }                                                                                                               \
+    static const hipError_t attr_err = hipFuncSetAttribute((const void*)gemv_scores_kernel<MODE, NQT>,              \
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); \
+    CMVE_HIP(attr_err);                                                                                             \
     hipLaunchKernelGGL((gemv_scores_kernel<MODE, NQT>), dim3(nblocks), dim3(256), lds, stream, qh, q->lo, gh, g->lo, \
                        g->d_pad, (int)q->n, g->n, ws, g->n_pad);                                                    \
   } while (0)

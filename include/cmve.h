@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 12
+#define CMVE_ABI_VERSION 13
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -394,25 +394,39 @@ int cmve_eval_graph_launch(cmve_handle_t h, cmve_eval_graph_t graph);
 int cmve_eval_graph_destroy(cmve_eval_graph_t graph);
 
 /*
- * Gallery-shard collectives over RCCL, for a host that shards the gallery
- * without torch.distributed (the Python mirror's cmve/dist.py runs the same exchange through
- * torch.distributed): every rank holds a resident shard; per batch the query rows are all-gathered,
- * each rank scores its shard (cmve_gt_thresholds / cmve_rank_count / cmve_topk), then the best-GT
- * scores are all-reduced MAX (NaN -> -inf marks "no GT in this shard") and the better-than-GT counts
- * SUM; top-k lists merge with cmve_merge_topk.  The reference never shards (LINAS-engine/evaluation.py:17-21
- * and inference.py:78-79 score one in-memory gallery); these replace nothing one-for-one.
- * RCCL (librccl.so) is opened with dlopen at first use.  cmve_dist_unique_id fills 128 bytes on ONE rank;
- * the host distributes them; cmve_dist_init binds a communicator of `nranks` to the handle (its device,
- * its stream for every collective; it makes the handle's device the calling thread's current device);
- * cmve_destroy releases it.
+ * Gallery-shard collectives over RCCL, for a C / C++ host that shards the
+ * gallery without torch.distributed.  (The Python host mirror, cmve/dist.py, runs the same exchange
+ * through torch.distributed -- backend "nccl" is RCCL -- and is the product path of bench.py; these
+ * entry points are its twin for hosts without torch.)  Every rank holds a resident shard; per batch the
+ * query rows are all-gathered, each rank scores its shard (cmve_gt_thresholds / cmve_rank_mfma +
+ * cmve_rank_fixup / cmve_topk), the best-GT scores are all-reduced MAX and the better-than-GT counts SUM,
+ * and the per-shard top-k runs are all-gathered and merged.  The reference never shards
+ * (LINAS-engine/evaluation.py:17-21 and inference.py:78-79 score one in-memory gallery); these replace
+ * nothing one-for-one.
+ * RCCL (librccl.so) is opened with dlopen at first use (thread-safe).  cmve_dist_unique_id fills 128 bytes
+ * on ONE rank; the host distributes them; cmve_dist_init binds a communicator of `nranks` to the handle
+ * (its device, its stream for every collective; it makes the handle's device the calling thread's current
+ * device); cmve_dist_destroy / cmve_destroy release it.
  * allgather_q: gathered[r * n_local + i] = rank r's local row i (n_local rows of d fp32 per rank).
- * reduce_rank: best_gt (fp64, in place, MAX) and / or counts (int32, in place, SUM), n entries each.
+ * reduce_rank: best_gt (fp64 [n], in place) in cmve_gt_thresholds' per-shard encoding -- NaN = no GT in
+ *   this shard, +inf = GTs in this shard that all score NaN, else the best finite score -- becomes the
+ *   global best-GT score in the same encoding (a finite score anywhere wins, then "all NaN", then "no GT":
+ *   the kernel maps NaN -> -inf and +inf -> -1e300 before the MAX and back after it, so RCCL never sees a
+ *   NaN); the result feeds cmve_rank_thresholds / cmve_gt_ranks unchanged.  counts (int32 [n], in place):
+ *   SUM.  Either pointer may be NULL.
+ * allgather_topk: every rank's exact local top-k (ids int64 [n_q, k] as GLOBAL gallery ids, -1 = empty
+ *   slot; scores fp64 [n_q, k]; each row sorted score desc / id asc) is gathered into the caller's
+ *   gathered_ids / gathered_scores (nranks * n_q * k each) and merged (as cmve_merge_topk) into
+ *   out [n_q, k_out] on every rank.  nranks <= 64.
  */
 #define CMVE_DIST_UNIQUE_ID_BYTES 128
 int cmve_dist_unique_id(void* id);
 int cmve_dist_init(cmve_handle_t h, int32_t nranks, int32_t rank, const void* id);
 int cmve_dist_allgather_q(cmve_handle_t h, const float* local, int64_t n_local, int64_t d, float* gathered);
 int cmve_dist_reduce_rank(cmve_handle_t h, double* best_gt, int32_t* counts, int64_t n);
+int cmve_dist_allgather_topk(cmve_handle_t h, const int64_t* ids, const double* scores, int64_t n_q, int32_t k,
+                             int64_t* gathered_ids, double* gathered_scores, int32_t k_out, int64_t* out_ids,
+                             double* out_scores);
 int cmve_dist_destroy(cmve_handle_t h);
 
 /*

@@ -1,11 +1,13 @@
-"""world_size-2 gloo rehearsal of the sharded-gallery protocol on CPU.
+"""world_size-2 gloo rehearsal of the sharded evaluation on CPU.
 
-Each rank scores its contiguous gallery shard with the ORACLE and does the shard-local steps (rank
-from the reduced counts, merge of the gathered runs) in numpy: those are HIP kernels in the product
-(cmve_gt_ranks, cmve_merge_topk) and are covered by the -m gpu tests.  Everything collective is the
-product coordination code of cmve.dist: all-gather of queries, the encoded all-reduce(MAX) of
-per-shard GT scores (NaN GTs included), all-reduce(SUM) of counts with the overflow flag, and the
-gather of the per-shard top-k runs.  Results must equal the unsharded oracle."""
+Every rank runs the PRODUCT coordination code of cmve.dist.ShardedGallery -- evaluate / cal_perf:
+the caption all-gather (uneven slices included), the encoded all-reduce(MAX) of per-shard t2v GT scores
+(NaN GTs included), the v2t direction ranked rank-locally against every gathered caption, ONE
+all-reduce(SUM) carrying the t2v counts + the v2t R@K sums + the overflow flag, the v2t rank gather and
+the mAP reduction.  Only the shard-local arithmetic (``_row_gt`` / ``_col_gt`` / ``_count`` / ``_ranks`` /
+``_positions``: HIP kernels in the product, covered by the -m gpu tests) is replaced here by the ORACLE,
+so the test runs on CPU.  Results must equal the unsharded oracle (ranks, and cal_perf's tuples against
+oracle.retrieval.cal_perf on the full error matrix)."""
 import os
 import socket
 
@@ -26,7 +28,99 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
+def _oracle_shard_class():
+    from cmve import dist as D
+
+    class OracleShard(D.ShardedGallery):
+        """ShardedGallery whose shard-local arithmetic is the fp64 oracle (test infrastructure)."""
+
+        def _setup(self, local_embs, with_lo, eps, device, with_f16, cap):
+            self.g = np.asarray(local_embs, np.float64)
+            self.n = self.g.shape[0]
+            self.device = torch.device("cpu")
+            self.eps = eps
+            self._s = None
+            self.grows = 0
+
+        def _pack(self, q_all, mode):
+            q = q_all.numpy() if torch.is_tensor(q_all) else np.asarray(q_all)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                self._s = R.exact_scores64(q, self.g)   # [n_q, n]
+            return q
+
+        def _csr(self, lists):
+            return [list(l) for l in lists]
+
+        @staticmethod
+        def _best(vals):
+            # cmve_gt_thresholds' per-shard encoding: NaN no GT, +inf every GT NaN, else the best
+            if vals.size == 0:
+                return np.nan
+            fin = vals[~np.isnan(vals)]
+            return fin.max() if fin.size else np.inf
+
+        def _row_gt(self, q, lists, mode):
+            return torch.tensor([self._best(self._s[i, l]) for i, l in enumerate(lists)], dtype=torch.float64)
+
+        def _col_gt(self, q, lists, mode):
+            return torch.tensor([self._best(self._s[l, j]) for j, l in enumerate(lists)], dtype=torch.float64), \
+                None, None
+
+        def _count(self, q, mode, sgt_row, col, events=None, chunks=1):
+            rc = cc = None
+            if sgt_row is not None:
+                t = sgt_row.numpy()
+                rc = torch.tensor([int(np.count_nonzero(self._s[i] > t[i])) if np.isfinite(t[i]) else 0
+                                   for i in range(self._s.shape[0])], dtype=torch.int32)
+            if col is not None:
+                t = col[0].numpy()
+                cc = torch.tensor([int(np.count_nonzero(self._s[:, j] > t[j])) if np.isfinite(t[j]) else 0
+                                   for j in range(self.n)], dtype=torch.int32)
+            return rc, cc, torch.tensor(False)
+
+        def _ranks(self, cnt, sgt, n, n_m):
+            c, s = cnt[:n].numpy().astype(np.int64), sgt[:n].numpy()
+            return torch.from_numpy(np.where(np.isnan(s), n_m + 1, np.where(np.isinf(s), n_m, c + 1)))
+
+        def _grow(self):
+            self.grows += 1
+
+        def _positions(self, q, lists, mode):
+            return [np.array([1 + int(np.count_nonzero(self._s[:, j] > self._s[k, j])) for k in l], np.int64)
+                    for j, l in enumerate(lists)]
+
+    return OracleShard
+
+
+def _problem(n_g, n_q, d, seed, multi_t2v):
+    rng = np.random.default_rng(seed)
+    gal = rng.standard_normal((n_g, d))
+    if multi_t2v:  # random GT lists: empty, single and multi-GT captions, NaN GTs
+        gts = [[int(x) for x in rng.choice(n_g, size=int(rng.integers(0, 3)), replace=False)] for _ in range(n_q)]
+        used = {int(x) for g in gts for x in g}
+        zero = [j for j in range(3, n_g, 7) if j not in used]
+        gal[zero] = 0.0
+        if n_g > 100:  # a zero GT video (a lone NaN GT: rank n_g) and a list mixing it with a finite GT
+            gal[4] = 0.0
+            gts[0], gts[1] = [4], [4, 50]
+        qs = gal[[g[0] if g else 0 for g in gts]] + 0.8 * rng.standard_normal((n_q, d))
+        v2t = [[] for _ in range(n_g)]
+        for i, l in enumerate(gts):
+            for g in l:
+                v2t[g].append(i)
+        return gal, qs, gts, v2t
+    # get_gt-shaped: one GT video per caption, several captions per video, some videos without captions
+    owner = rng.integers(0, n_g, n_q)
+    zero = [j for j in range(5, n_g, 11) if j not in set(owner.tolist())]
+    gal[zero] = 0.0  # zero videos without captions: NaN columns, empty v2t lists
+    qs = gal[owner] + 0.8 * rng.standard_normal((n_q, d))
+    vid = [f"video{j}" for j in range(n_g)]
+    cid = [f"video{int(o)}#{i}" for i, o in enumerate(owner)]
+    v2t, t2v = R.get_gt(vid, cid)
+    return gal, qs, t2v, v2t
+
+
+def _worker(rank, world, port, n_g, n_q, d, k, q_split, multi_t2v, result_q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "cross-modal-video-engine_amd"))
@@ -34,78 +128,74 @@ def _worker(rank, world, port, n_g, n_q, d, k, q_per_rank, result_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from cmve import dist as D  # coordination helpers only (no GPU needed)
-        rng = np.random.default_rng(11)
-        gal = rng.standard_normal((n_g, d))
-        gts = [list(rng.choice(n_g, size=int(rng.integers(0, 3)), replace=False)) for _ in range(n_q)]
-        used = {int(x) for g in gts for x in g}
-        zero = [j for j in range(3, n_g, 7) if j not in used]
-        gal[zero] = 0.0  # zero videos (never a GT): NaN scores, ranked last
-        if n_g > 100:  # a zero GT video (a lone NaN GT: rank n_g) and a list mixing it with a finite GT
-            gal[4] = 0.0
-            gts[0], gts[1] = [4], [4, 50]
-        qs = gal[[g[0] if g else 0 for g in gts]] + 0.8 * rng.standard_normal((n_q, d))
+        from cmve import dist as D  # coordination code (no GPU needed: the local arithmetic is the oracle)
+        gal, qs, t2v, v2t = _problem(n_g, n_q, d, 11 + n_g, multi_t2v)
         lo, hi = D.shard_bounds(n_g, world, rank)
-        # each rank contributes its query slice; all-gather restores the global order
-        q_local = torch.from_numpy(qs[rank * q_per_rank:(rank + 1) * q_per_rank].copy())
-        q_all = torch.empty((world * q_per_rank, d), dtype=q_local.dtype)
-        work = D.gather_rows_async(q_local, q_all, world)  # the bench's overlapped form
-        work.wait()
-        assert np.array_equal(q_all.numpy(), qs)
-        assert bool(D.any_flag(torch.tensor(rank == 1), world)) and not bool(D.any_flag(torch.tensor(False), world))
-        s = R.exact_scores64(q_all.numpy(), gal[lo:hi])             # local shard scores (oracle)
-        local = D.local_gt_lists(gts, lo, hi)
-        def shard_sgt(i, l):  # cmve_gt_thresholds' per-shard encoding: NaN none, +inf all-NaN
-            if not l:
-                return np.nan
-            v = s[i, l]
-            return v[~np.isnan(v)].max() if (~np.isnan(v)).any() else np.inf
-        sgt = torch.tensor([shard_sgt(i, l) for i, l in enumerate(local)], dtype=torch.float64)
-        sgt = D.merge_gt_scores(sgt, world)
-        cnt = torch.tensor([int(np.count_nonzero(s[i] > sgt[i].item())) if np.isfinite(sgt[i].item()) else 0
-                            for i in range(n_q)], dtype=torch.int32)
-        flag = torch.tensor([1 if rank == 1 else 0], dtype=torch.int32)  # one rank's overflow reaches all
-        both = D.reduce_counts(torch.cat([cnt, flag]), world)
-        cnt, ovf = both[:-1], int(both[-1])
-        assert ovf == 1
-        sg = sgt.numpy()
-        ranks = np.where(np.isnan(sg), n_g + 1, np.where(np.isinf(sg), n_g, cnt.numpy().astype(np.int64) + 1))
-        rc = D.recall_counts_device(torch.from_numpy(ranks)).tolist()
-        assert rc == [int((ranks <= 1).sum()), int((ranks <= 5).sum()), int((ranks <= 10).sum()), int(ranks.sum())]
+        qlo, qhi = q_split[rank], q_split[rank + 1]  # uneven caption slices are gathered in rank order
+        q_local = torch.from_numpy(qs[qlo:qhi].copy())
+        comm = D.TorchComm()
+        assert comm.world == world and comm.rank == rank
+        # collectives of the bench's overlapped form
+        q_eq = torch.from_numpy(qs[rank * (n_q // world):(rank + 1) * (n_q // world)].copy())
+        q_all = torch.empty((n_q // world * world, d), dtype=q_eq.dtype)
+        D.gather_rows_async(q_eq, q_all, comm).wait()
+        assert np.array_equal(q_all.numpy(), qs[:q_all.shape[0]])
+        assert bool(D.any_flag(torch.tensor(rank == 1), comm)) and not bool(D.any_flag(torch.tensor(False), comm))
+        assert np.array_equal(D.all_gather_var(q_local, comm).numpy(), qs)
+        shard = _oracle_shard_class()(gal[lo:hi], offset=lo, n_global=n_g, comm=comm)
+        t2v_lists = [t2v[i] for i in range(n_q)]
+        r_t, r_v = shard.evaluate(q_local, t2v_lists, v2t)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            s_full = R.exact_scores64(qs, gal)
+        ok = {"t2v": bool(np.array_equal(r_t, R.rank_counts(s_full, t2v_lists))),
+              "v2t": bool(np.array_equal(r_v, R.rank_counts(s_full.T, v2t)))}
+        # the one-collective device step: v2t R@K sums of all shards ride the t2v counts' all-reduce
+        q = shard._pack(D.all_gather_var(q_local, comm), 0)
+        _, v_loc, rec, ovf = shard.evaluate_device(torch.from_numpy(q), shard.local_gt_csr(t2v_lists),
+                                                   shard.local_v2t_csr(v2t), n_q)
+        ok["v2t_recall_sums"] = rec.tolist() == [int((r_v <= 1).sum()), int((r_v <= 5).sum()),
+                                                 int((r_v <= 10).sum()), int(r_v.sum())]
+        ok["v2t_local"] = bool(np.array_equal(v_loc.numpy(), r_v[lo:hi])) and not bool(ovf)
+        if not multi_t2v:
+            got = shard.cal_perf(q_local, v2t, t2v)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                exp = R.cal_perf(-s_full, v2t, t2v)
+            ok["cal_perf"] = all(np.allclose(np.asarray(g, float), np.asarray(e, float), rtol=0, atol=1e-12)
+                                 for g, e in zip(got, exp))
+        # top-k: each shard's exact local top-k with global ids, gathered in the merge kernel's layout
+        with np.errstate(invalid="ignore", divide="ignore"):
+            s = R.exact_scores64(qs, gal[lo:hi])
         kk = min(k, hi - lo)
         order = np.argsort(-s, axis=1, kind="stable")[:, :kk]
-        idx_g = torch.from_numpy(order + lo)
-        sc = torch.from_numpy(np.take_along_axis(s, order, axis=1))
-        idx_g, sc = D.pad_topk(idx_g, sc, k)
-        gi, gs = D.gather_topk(idx_g, sc, world)
+        idx_g, sc = D.pad_topk(torch.from_numpy(order + lo), torch.from_numpy(np.take_along_axis(s, order, 1)), k)
+        gi, gs = D.gather_topk(idx_g, sc, comm)
         assert gi.shape == (n_q, world * k)
         top = np.empty((n_q, k), np.int64)
         for i in range(n_q):  # merge of the gathered runs (cmve_merge_topk on the GPU)
             ids, scs = gi[i].numpy(), gs[i].numpy()
             keep = ids >= 0
-            o = np.lexsort((ids[keep], -scs[keep]))[:k]
+            o = np.lexsort((ids[keep], -np.nan_to_num(scs[keep], nan=-np.inf)))[:k]
             top[i] = ids[keep][o]
+        ok["topk"] = bool(np.array_equal(top, np.argsort(-s_full, axis=1, kind="stable")[:, :k]))
         if rank == 0:
-            s_full = R.exact_scores64(qs, gal)
-            exp_ranks = R.rank_counts(s_full, gts)
-            exp_top = np.argsort(-s_full, axis=1, kind="stable")[:, :k]
-            result_q.put((bool(np.array_equal(ranks, exp_ranks)), bool(np.array_equal(top, exp_top))))
+            result_q.put(ok)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_g", [9, 301, 512])
-def test_sharded_protocol_world2(n_g):
+@pytest.mark.parametrize("n_g,multi_t2v", [(9, True), (301, True), (512, True), (64, False), (301, False)])
+def test_sharded_evaluation_world2(n_g, multi_t2v):
     world, n_q, d, k = 2, 40, 24, 7
     ctx = mp.get_context("spawn")
     result_q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_g, n_q, d, k, n_q // world, result_q))
+    split = (0, 23, n_q)  # uneven caption slices
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_g, n_q, d, k, split, multi_t2v, result_q))
              for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=180)
         assert p.exitcode == 0
-    ranks_ok, top_ok = result_q.get()
-    assert ranks_ok and top_ok
+    ok = result_q.get()
+    assert all(ok.values()), ok
