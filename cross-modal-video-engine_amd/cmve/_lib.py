@@ -75,6 +75,7 @@ SIGNATURES = {
     "cmve_combine_train_fwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp]),
     "cmve_combine_train_bwd": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
     "cmve_pool_mean_bwd": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp]),
+    "cmve_tsn_pool": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64]),
     "cmve_adaptive_avg_pool2d": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp]),
     "cmve_layernorm": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _i64]),
     "cmve_mha_1q": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64]),

@@ -447,6 +447,9 @@ class RankSession:
         self.ws = torch.zeros(nbytes.value, dtype=torch.uint8, device=self.device)  # zeroed once (ABI contract)
         self.cap = int(cap)
         self._args = None
+        # captured graphs bake the workspace address in: a new workspace makes them stale (EvalGraph.launch
+        # refuses them), and each graph keeps the workspace it was captured with alive
+        self._ws_gen = getattr(self, "_ws_gen", -1) + 1
 
     @property
     def ncand(self) -> int:
@@ -470,9 +473,13 @@ class RankSession:
         return src
 
     def enqueue(self, captions, videos, timing_slot: int = -1, out: Optional[torch.Tensor] = None,
-                _bind_only: bool = False):
-        """Enqueue one evaluation on the current stream (no synchronisation).  The inputs must stay
-        alive and unmodified until it completes.  out: optional int64 device tensor of
+                _bind_only: bool = False, wait_current: bool = True):
+        """Enqueue one evaluation (no host synchronisation) on the session's stream, or on the current
+        stream without one.  The inputs must stay unmodified until it completes.  With a session stream the
+        evaluation first waits for the work already enqueued on the caller's current stream (the producer of
+        the embeddings, e.g. an encoder), and inputs read in place are recorded on the session stream for
+        the caching allocator; ``wait_current=False`` skips the wait for callers whose inputs are known to
+        be complete (a resident buffer the caller synchronised once).  out: optional int64 device tensor of
         ``EVAL_OUT_HEAD + n_q + n_g`` words receiving this evaluation's head + ranks instead of
         ``self.out`` (a ring of them lets pipelined evaluations be read back in batches)."""
         if out is None:
@@ -486,8 +493,15 @@ class RankSession:
             # (re)bind: the same input tensors again (a resident buffer refilled between evaluations)
             # reuse the bound descriptors and the prepared argument tuple -- the host side of an
             # evaluation is then one ctypes call
+            if self.stream is not None and wait_current:
+                self._order_after_current()
+                wait_current = False
             with self._ctx():  # a copying bind goes on the session's stream
                 self._bound = (self._bind(self.q, captions), self._bind(self.g, videos))
+            if self.stream is not None:  # read in place on another stream: keep the allocator from reusing them early
+                for x, b in zip((captions, videos), self._bound):
+                    if torch.is_tensor(x) and b is x:
+                        x.record_stream(self.stream)
             if self._bound[0] is not captions or self._bound[1] is not videos:
                 self._bound = (None, None)  # copied into the session's own buffers: rebind next time
             r = self.row if self.row is not None else (None, None)
@@ -496,8 +510,16 @@ class RankSession:
                           _ptr(c[1]), _ptr(self.ws), self.ws.numel(), self.cap)
         if _bind_only:
             return
+        if self.stream is not None and wait_current:
+            self._order_after_current()
         h = self._h if self._h is not None else handle(self.device)
         check(lib.cmve_eval_ranks(h, *self._args, _ptr(out), int(timing_slot)), "cmve_eval_ranks")
+
+    def _order_after_current(self):
+        """The session stream waits for the work enqueued so far on the caller's current stream."""
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != self.stream.cuda_stream:
+            self.stream.wait_stream(cur)
 
     def graph(self, captions, videos, out: Optional[torch.Tensor] = None) -> "EvalGraph":
         """One evaluation of these inputs into `out` (default self.out) captured into a HIP graph on the
@@ -514,7 +536,7 @@ class RankSession:
         h = self._h if self._h is not None else handle(self.device)
         gh = C.c_void_p()
         check(lib.cmve_eval_graph_create(h, *self._args, _ptr(out), C.byref(gh)), "cmve_eval_graph_create")
-        return EvalGraph(gh.value, h, (captions, videos, out, self))
+        return EvalGraph(gh.value, h, (captions, videos, out, self, self.ws), self, self._ws_gen)
 
     def timing(self, slot: int):
         """(pack+thresholds, rank GEMM, fix-up+ranks) milliseconds of the evaluation that used `slot`."""
@@ -547,10 +569,22 @@ class EvalGraph:
     """A captured RankSession evaluation (cmve_eval_graph_*): ``launch()`` enqueues it on the session's
     stream with one host call.  Keeps its inputs, output and session alive."""
 
-    def __init__(self, gh: int, h: int, keep):
-        self._g, self._h, self._keep = gh, h, keep
+    def __init__(self, gh: int, h: int, keep, session: Optional["RankSession"] = None, ws_gen: int = 0):
+        self._g, self._h, self._keep = gh, h, keep  # keep: inputs, output, session and the captured workspace
+        self._session, self._ws_gen = session, ws_gen
+
+    @property
+    def stale(self) -> bool:
+        """True once the session replaced its workspace (an overflow in run()): the graph's baked-in
+        undecided-pair list is no longer the session's, and its capacity is the one that overflowed."""
+        return self._session is not None and self._session._ws_gen != self._ws_gen
 
     def launch(self):
+        if not self._g:
+            raise RuntimeError("EvalGraph.launch: the graph was closed")
+        if self.stale:
+            raise RuntimeError("EvalGraph.launch: the session's workspace was regrown after this graph was "
+                               "captured; capture a new graph (RankSession.graph)")
         check(lib.cmve_eval_graph_launch(self._h, self._g), "cmve_eval_graph_launch")
 
     def close(self):

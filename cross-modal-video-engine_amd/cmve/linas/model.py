@@ -74,12 +74,17 @@ class _PackedWeight:
 
 
 def linear_fused(x: torch.Tensor, weight: torch.Tensor, bias=None, relu=False, resid=None, bn=None,
-                 packed: _PackedWeight = None) -> torch.Tensor:
-    """out = BN(resid + act(x W^T + b)) on the split-bf16 MFMA kernel (K3)."""
+                 packed: _PackedWeight = None, out: torch.Tensor = None) -> torch.Tensor:
+    """out = BN(resid + act(x W^T + b)) on the split-bf16 MFMA kernel (K3); `out` (fp32 [n, F_out], rows
+    contiguous, any row stride) receives it in place when given."""
     x = x.detach().float().contiguous()
     xr = engine.RowSet(x, with_lo=True, with_f16=False, raw_rows=True, device=x.device)
     wr = (packed or _PackedWeight()).get(weight)
-    out = torch.empty((x.shape[0], weight.shape[0]), dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty((x.shape[0], weight.shape[0]), dtype=torch.float32, device=x.device)
+    elif (out.dtype != torch.float32 or tuple(out.shape) != (x.shape[0], weight.shape[0]) or out.stride(1) != 1
+          or out.device != x.device):
+        raise ValueError(f"linear_fused: out must be fp32 [{x.shape[0]}, {weight.shape[0]}] on {x.device}")
     scale = shift = None
     if bn is not None:
         scale, shift = bn

@@ -138,9 +138,90 @@ __global__ __launch_bounds__(256) void adaptive_avg_kernel(const float* __restri
   }
 }
 
+// TSN feature-extraction head (MCT/mmaction/models/recognizers/recognizer2d.py:76-83): backbone maps
+// x[B*S, C, HW] (NCHW, HW = H*W) -> AdaptiveAvgPool2d(1) per plane -> reshape (B, S, C) -> mean over S.
+// Block = (64-channel group, video b), 4 waves; wave w takes segments s = w, w+4, ...: it copies the
+// segment's contiguous [64 x HW] tile into its own LDS slab with float4 loads (row stride HW + 1: the
+// per-channel reads below are conflict-free), then lane c sums plane c in hw order (fp32) and adds
+// plane_sum / HW to its running segment sum.  The 4 wave partials are combined in wave order.
+constexpr int TSN_CH = 64;
+constexpr int TSN_MAX_HW = 128;  // LDS: 4 waves x 64 x (HW + 1) floats <= 129 KiB
+
+__global__ __launch_bounds__(256) void tsn_pool_kernel(const float* __restrict__ x, int64_t S, int64_t C, int64_t HW,
+                                                       float* __restrict__ out, int64_t ldo, int vec) {
+  extern __shared__ float tsn_lds[];
+  __shared__ float red[4][TSN_CH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.y, c0 = (int64_t)blockIdx.x * TSN_CH;
+  const int64_t nch = C - c0 < TSN_CH ? C - c0 : TSN_CH;
+  const int hw = (int)HW, tile = (int)(nch * HW);  // <= 64 * 128
+  const float inv_hw = 1.f / (float)hw;
+  // k -> (channel, position) without an integer divide: a float estimate, corrected by one step
+  auto slab_at = [&](int k) {
+    int ch = (int)((float)k * inv_hw);
+    ch += (ch + 1) * hw <= k ? 1 : 0;
+    ch -= ch * hw > k ? 1 : 0;
+    return ch * (hw + 1) + (k - ch * hw);
+  };
+  float* slab = tsn_lds + w * TSN_CH * (hw + 1);
+  float acc = 0.f;
+  for (int64_t s = w; s < S; s += 4) {
+    const float* src = x + ((b * S + s) * C + c0) * HW;
+    if (vec) {  // src 16-byte aligned and tile % 4 == 0 (checked on the host)
+      for (int i = lane * 4; i < tile; i += 256) {
+        const f32x4_t v = *(const f32x4_t*)(src + i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) slab[slab_at(i + e)] = v[e];
+      }
+    } else {
+      for (int k = lane; k < tile; k += 64) slab[slab_at(k)] = src[k];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes are done (the slab is wave-private)
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nch) {
+      float p = 0.f;
+      for (int k = 0; k < hw; ++k) p += slab[lane * (hw + 1) + k];
+      acc += p / (float)hw;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && lane < nch) {
+    const float r = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    out[b * ldo + c0 + lane] = r / (float)S;
+  }
+}
+
 }  // namespace cmve
 
 using namespace cmve;
+
+extern "C" int cmve_tsn_pool(cmve_handle_t h, const float* x, int64_t B, int64_t S, int64_t C, int64_t HW, float* out,
+                             int64_t ldo) {
+  CMVE_REQUIRE(h && out && (B == 0 || x), "cmve_tsn_pool: NULL argument");
+  CMVE_REQUIRE(B >= 0 && S > 0 && C > 0 && HW > 0 && ldo >= C, "cmve_tsn_pool: bad shape");
+  CMVE_REQUIRE(HW <= TSN_MAX_HW, "cmve_tsn_pool: H*W = %lld > %d (pool the maps spatially first)", (long long)HW,
+               TSN_MAX_HW);
+  CMVE_REQUIRE(B <= 65535, "cmve_tsn_pool: B = %lld > 65535 videos per call", (long long)B);
+  if (B == 0) return CMVE_OK;
+  if (HW == 1) {  // maps already pooled spatially: [B, S, C] -> the MEAN_ALL temporal pool
+    dim3 grid((unsigned)((C + 255) / 256), (unsigned)B);
+    hipLaunchKernelGGL(pool_kernel<1>, grid, dim3(256), 0, h->stream, x, S * C, C, S, C, (const int32_t*)nullptr, out,
+                       ldo);
+    return check_launch("pool_kernel");
+  }
+  const int vec = ((uintptr_t)x % 16 == 0) && (C * HW) % 4 == 0 && (HW % 4 == 0 || C % TSN_CH == 0);
+  const size_t lds = 4 * (size_t)TSN_CH * (size_t)(HW + 1) * sizeof(float);
+  static const hipError_t attr_err =
+      hipFuncSetAttribute((const void*)tsn_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TSN_CH *
+                                                                                                      (TSN_MAX_HW + 1) *
+                                                                                                      (int)sizeof(float));
+  CMVE_HIP(attr_err);
+  dim3 grid((unsigned)((C + TSN_CH - 1) / TSN_CH), (unsigned)B);
+  hipLaunchKernelGGL(tsn_pool_kernel, grid, dim3(256), lds, h->stream, x, S, C, HW, out, ldo, vec);
+  return check_launch("tsn_pool_kernel");
+}
 
 extern "C" int cmve_adaptive_avg_pool2d(cmve_handle_t h, const float* x, int64_t P, int64_t H, int64_t W,
                                         int64_t sp, int64_t sh, int64_t OH, int64_t OW, float* out) {

@@ -162,6 +162,14 @@ int cmve_temporal_pool(cmve_handle_t h, const float* x, int64_t stride_b, int64_
                        int64_t B, int64_t T, int64_t F, const int32_t* lengths, int32_t mode,
                        float* out, int64_t ldo);
 
+/* K2 -- TSN feature-extraction head (MCT/mmaction/models/recognizers/recognizer2d.py:76-83, the
+ * feature_extraction branch of Recognizer2D.forward_test): x = the backbone's maps [B * S, C, H, W]
+ * (NCHW, contiguous; HW = H * W <= 128; HW = 1 for maps already pooled spatially, i.e. [B, S, C])
+ * -> AdaptiveAvgPool2d(1) -> reshape (B, S, C) -> mean over the S segments -> out [B, C] (row
+ * stride ldo).  fp32, plane sums in hw order.  B <= 65535 per call. */
+int cmve_tsn_pool(cmve_handle_t h, const float* x, int64_t B, int64_t S, int64_t C, int64_t HW, float* out,
+                  int64_t ldo);
+
 /* K2 -- F.adaptive_avg_pool2d of the reference video's middle tokens before the single-query
  * combine (MultiFusion/src/inference.py:58-59: [1, T, 18*18, C] -> [1, T, 16, D]).
  * x: P planes of [H, W] fp32 (plane stride sp, row stride sh, columns contiguous);

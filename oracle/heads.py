@@ -46,6 +46,18 @@ def pool_mean(x):
     return np.mean(x, axis=1)
 
 
+def tsn_feature_extraction(x, batches):
+    """MCT/mmaction/models/recognizers/recognizer2d.py:76-83 (feature_extraction=True): the backbone maps
+    x [batches * num_segs, C, H, W] -> AdaptiveAvgPool2d(1) (:78-79, a mean over H x W per plane) ->
+    reshape (batches, num_segs, -1) (:81) -> mean over axis 1 (:83).  fp64.  MCT is not importable here
+    (mmcv is absent): pinned against torch's own AdaptiveAvgPool2d + mean on the same maps
+    (tests/test_oracle_heads.py), parity with a run of the reference itself unpinned."""
+    x = np.asarray(x, np.float64)
+    n, C = x.shape[:2]
+    planes = x.reshape(n, C, -1).mean(axis=2)
+    return planes.reshape(batches, n // batches, C).mean(axis=1)
+
+
 def l2norm(x):
     """LINAS-engine/model.py:35-40 (no epsilon)."""
     return x / np.sqrt(np.sum(x * x, axis=1, keepdims=True))

@@ -59,6 +59,15 @@ def test_pair_losses_match_torch(kind, name, reduction):
         assert torch.isnan(ln)
         ln.backward()
         torch.testing.assert_close(xn.grad, -yn)
+        # the target gradient where the target is 0 or negative (the reference's model.py:878/880 pass a
+        # target that requires grad): torch's kl_div is xlogy(t, t) - t * x, whose autograd gives
+        # log(t) + t / t - x -- NaN at t == 0 as well as t < 0 (torch 1.9's fused backward masked t == 0
+        # to 0; the goldens are made with this container's torch, which we follow)
+        yg = yn.detach().clone().requires_grad_(True)
+        DL.KLDivLoss(reduction="sum")(xn.detach(), yg).backward()
+        yc = yn.detach().cpu().clone().requires_grad_(True)
+        torch.nn.KLDivLoss(reduction="sum")(xn.detach().cpu(), yc).backward()
+        torch.testing.assert_close(yg.grad.cpu(), yc.grad, equal_nan=True)
 
 
 def _heads(g, pre):

@@ -610,3 +610,43 @@ def test_rank_session_graph_replays(torch_cuda):
     assert np.array_equal(ring[1, H + nq:H + nq + ng].cpu().numpy(), c2)
     for gr in graphs:
         gr.close()
+    # a regrown workspace (an overflow in run()) makes every graph captured before it stale: launching one
+    # would write into the replaced buffer, so launch() refuses it; a new capture works
+    g_old = sess.graph(q_t, g_t, out=ring[0])
+    sess._alloc(600)
+    r3, c3 = sess.run(q_t, g_t)
+    assert g_old.stale and np.array_equal(r3, r2) and np.array_equal(c3, c2)
+    with pytest.raises(RuntimeError, match="regrown"):
+        g_old.launch()
+    g_new = sess.graph(q_t, g_t, out=ring[2])
+    g_new.launch()
+    st.synchronize()
+    assert np.array_equal(ring[2, H:H + nq].cpu().numpy(), r2)
+    g_new.close()
+    g_old.close()
+
+
+def test_rank_session_stream_waits_for_the_producer(torch_cuda):
+    """RankSession(stream=...) orders each evaluation after the work already on the caller's current stream:
+    inputs written there behind a long-running kernel are read complete, with no manual synchronisation."""
+    import torch
+    from cmve import engine
+    rng = np.random.default_rng(13)
+    nq, ng, d = 400, 800, 256
+    gal = rng.standard_normal((ng, d))
+    qs = gal[rng.integers(0, ng, nq)] + 2.0 * rng.standard_normal((nq, d))
+    row_gts = [[int(x)] for x in rng.integers(0, ng, nq)]
+    s = R.exact_scores64(qs, gal)
+    exp = R.rank_counts(s, row_gts)
+    sess = engine.RankSession(nq, ng, d, row_gts=row_gts, dtype=torch.float64, stream=torch.cuda.Stream())
+    src_q, src_g = torch.from_numpy(qs).cuda(), torch.from_numpy(gal).cuda()
+    torch.cuda.synchronize()
+    for rep in range(3):
+        q_t = torch.zeros_like(src_q)   # allocated and written on the current (default) stream ...
+        g_t = torch.zeros_like(src_g)
+        torch.cuda._sleep(20_000_000)   # ... behind a ~10 ms spin
+        q_t.copy_(src_q)
+        g_t.copy_(src_g)
+        t2v, _ = sess.run(q_t, g_t)     # no torch.cuda.synchronize() in between
+        assert np.array_equal(t2v, exp), rep
+

@@ -57,3 +57,16 @@ def test_infonce(golden, B):
     np.testing.assert_allclose([row, col], [g["row"], g["col"]], rtol=1e-5)
     for a, b in ((dPr, "dP_row"), (dTr, "dT_row"), (dPc, "dP_col"), (dTc, "dT_col")):
         np.testing.assert_allclose(a, g[b], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("shape", [(3, 25, 32, 8, 8), (2, 3, 16, 7, 7), (4, 5, 8, 1, 1)])
+def test_tsn_feature_extraction_against_torch_ops(shape):
+    """MCT recognizer2d.py:76-83 restated (oracle.heads.tsn_feature_extraction) == the torch ops the
+    reference calls there (nn.AdaptiveAvgPool2d(1), reshape, mean(axis=1)) on the same maps, in fp64.
+    (MCT needs mmcv, absent: this pins the restatement to the ops, not to a run of the module.)"""
+    import torch
+    B, S, C, H_, W = shape
+    x = np.random.default_rng(sum(shape)).standard_normal((B * S, C, H_, W))
+    xt = torch.from_numpy(x)
+    ref = torch.nn.AdaptiveAvgPool2d(1)(xt).reshape((B, S, -1)).mean(axis=1).numpy()
+    np.testing.assert_allclose(H.tsn_feature_extraction(x, B), ref, rtol=0, atol=1e-14)
