@@ -27,6 +27,7 @@ TOPK_MAX = 2048
 MAX_CHUNKS = 16
 EVAL_TIMING_SLOTS = 32
 EVAL_OUT_HEAD = 16
+EVAL_PAIRED = 0x100  # CMVE_EVAL_PAIRED
 DIST_UNIQUE_ID_BYTES = 128  # CMVE_DIST_UNIQUE_ID_BYTES
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
@@ -99,6 +100,7 @@ SIGNATURES = {
     "cmve_eval_workspace": (C.c_int, [_P(Rows), _P(Rows), _i64, _P(_i64)]),
     "cmve_eval_ranks": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _i32]),
     "cmve_eval_timing": (C.c_int, [_vp, _i32, _P(_f32)]),
+    "cmve_eval_kernel_timing": (C.c_int, [_vp, _i32, _P(_f32)]),
     "cmve_eval_graph_create": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp,
                                          _P(_vp)]),
     "cmve_eval_graph_launch": (C.c_int, [_vp, _vp]),

@@ -428,6 +428,9 @@ class RankSession:
                         with_f16=(mode == _lib.SIM_F16), device=dev)
         self.row = csr(row_gts, dev) if row_gts is not None else None
         self.col = csr(col_gts, dev) if col_gts is not None else None
+        # a one-to-one GT pairing (MSR-VTT-1kA: caption i <-> video p(i)) lets the evaluation's prep pack and
+        # score each (caption, video) pair in one wave (CMVE_EVAL_PAIRED)
+        self.paired = self._is_pairing(row_gts, col_gts, n_q, n_g)
         self._alloc(int(cand_cap) if cand_cap else max(1 << 16, 64 * (n_q + n_g)))
         self.out = torch.zeros(_lib.EVAL_OUT_HEAD + n_q + n_g, dtype=torch.int64, device=dev)
         self.host = torch.zeros(_lib.EVAL_OUT_HEAD + n_q + n_g, dtype=torch.int64).pin_memory()
@@ -436,6 +439,16 @@ class RankSession:
         # current-stream switch per evaluation: ~6 us of host time each); None = the caller's current stream
         self.stream = stream
         self._h = stream_handle(dev, stream) if stream is not None else None
+
+    @staticmethod
+    def _is_pairing(row_gts, col_gts, n_q, n_g) -> bool:
+        if row_gts is None or col_gts is None or n_q != n_g:
+            return False
+        rows = [row_gts[i] for i in range(n_q)]
+        cols = [col_gts[j] for j in range(n_g)]
+        if any(len(l) != 1 for l in rows) or any(len(l) != 1 for l in cols):
+            return False
+        return all(0 <= int(rows[i][0]) < n_g and int(cols[int(rows[i][0])][0]) == i for i in range(n_q))
 
     def _ctx(self):
         return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
@@ -506,7 +519,8 @@ class RankSession:
                 self._bound = (None, None)  # copied into the session's own buffers: rebind next time
             r = self.row if self.row is not None else (None, None)
             c = self.col if self.col is not None else (None, None)
-            self._args = (C.byref(self.q.desc), C.byref(self.g.desc), self.mode, _ptr(r[0]), _ptr(r[1]), _ptr(c[0]),
+            mode = self.mode | (_lib.EVAL_PAIRED if self.paired else 0)
+            self._args = (C.byref(self.q.desc), C.byref(self.g.desc), mode, _ptr(r[0]), _ptr(r[1]), _ptr(c[0]),
                           _ptr(c[1]), _ptr(self.ws), self.ws.numel(), self.cap)
         if _bind_only:
             return
@@ -543,6 +557,14 @@ class RankSession:
         ms = (C.c_float * 3)()
         h = self._h if self._h is not None else handle(self.device)
         check(lib.cmve_eval_timing(h, int(slot), ms), "cmve_eval_timing")
+        return list(ms)
+
+    def kernel_timing(self, slot: int):
+        """(prep, rank GEMM, fix-up, finish) kernel durations in ms of the evaluation that used `slot`, each
+        from its launch's own start / stop (the durations rocprofv3 reports)."""
+        ms = (C.c_float * 4)()
+        h = self._h if self._h is not None else handle(self.device)
+        check(lib.cmve_eval_kernel_timing(h, int(slot), ms), "cmve_eval_kernel_timing")
         return list(ms)
 
     def run(self, captions, videos):

@@ -13,6 +13,7 @@
 namespace cmve {
 
 static thread_local std::string g_last_error;
+thread_local LaunchEv g_launch_ev;
 
 void set_error(const char* fmt, ...) {
   char buf[1024];
@@ -187,6 +188,12 @@ int cmve_destroy(cmve_handle_t h) {
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->tev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& slot : h->eval_ev)
+      for (hipEvent_t e : slot)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& slot : h->eval_kev)
+      for (hipEvent_t e : slot)
+        if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
   }
   delete h;

@@ -1,6 +1,7 @@
 // Internal helpers shared by the libcmve.so translation units (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <math.h>
 #include <string>
@@ -18,6 +19,8 @@ struct cmve_handle {
   int last_chunks = 0;
   // timing events of cmve_eval_ranks (a ring of CMVE_EVAL_TIMING_SLOTS x 4, created on first use)
   hipEvent_t eval_ev[CMVE_EVAL_TIMING_SLOTS][4] = {};
+  // kernel-exact timing of the same evaluations: start / stop of each of the four launches
+  hipEvent_t eval_kev[CMVE_EVAL_TIMING_SLOTS][8] = {};
   // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -37,6 +40,23 @@ void dist_release(cmve_handle* h);
 // k-way merge of sorted top-k runs (merge.hip): entry (q, run l, pos p) at q * q_stride + l * l_stride + p
 int merge_topk_launch(hipStream_t s, const int64_t* ids, const double* scores, int64_t n_q, int lists, int k_in,
                       int64_t q_stride, int64_t l_stride, int k_out, int64_t* out_ids, double* out_scores);
+// Kernel-exact launch timing: when armed, the next launch made through cmve::launch records its own start
+// and stop on these events (hipExtLaunchKernelGGL: the dispatch's timestamps, the duration rocprofv3
+// reports -- events recorded around a launch also count its dispatch gap)
+struct LaunchEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local LaunchEv g_launch_ev;
+template <typename F, typename... Args>
+inline void launch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+  if (g_launch_ev.start) {
+    const LaunchEv e = g_launch_ev;
+    g_launch_ev = LaunchEv{};
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, e.start, e.stop, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+  }
+}
 // compute units of the current device (queried once per device; thread-safe)
 int device_cus();
 

@@ -23,42 +23,48 @@
 
 namespace cmve {
 
-// prep_row for rows of <= 1024 elements that both sides read in 16-B pieces (rows_vec4): the row is
-// loaded ONCE into registers (16 doubles per lane, elements 4L + 256m + c) and packed from there, and
-// each GT partner is read once for both its sum of squares and the dot product.  Every per-lane
-// accumulation runs in the (m, c) order of row_sumsq / pack_row_planes / wave_dot64, so the planes,
-// bounds, norms and GT scores are bit-identical to the streaming path (and to cmve_pack_rows /
-// cmve_gt_thresholds).
-template <typename TA, typename TB>
-__device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide& B, const EvalCommon& c, int64_t row,
-                                              const TA* __restrict__ x, uint16_t* hrow, uint16_t* lrow,
-                                              uint16_t* frow, int lane, float (&eb)[3]) {
-  // the first GT partner's row is loaded beside the row itself (its index is known up front): the
-  // GT score then needs no second HBM round trip after the pack
-  const int64_t g_beg = A.off ? A.off[row] : 0, g_end = A.off ? A.off[row + 1] : 0;
-  double w0[4][4];
-  if (g_beg < g_end) {
-    const TB* y = (const TB*)B.raw + (int64_t)A.idx[g_beg] * B.ld;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int64_t k = (int64_t)lane * 4 + 256 * m;
-      if (k < c.d) load4d(y + k, w0[m]);
-    }
-  }
-  double v[4][4];
+// The register-resident pieces of the prep for rows of <= 1024 elements that both sides read in 16-B
+// pieces (rows_vec4): a row is loaded ONCE into registers (16 doubles per lane, elements 4L + 256m + c)
+// and normalised, packed and dotted from there.  Every per-lane accumulation runs in the (m, c) order of
+// row_sumsq / pack_row_planes / wave_dot64, so the planes, bounds, norms and GT scores are bit-identical
+// to the streaming path (and to cmve_pack_rows / cmve_gt_thresholds).
+template <typename T>
+__device__ __forceinline__ void load_row_regs(const T* __restrict__ x, int64_t d, int lane, double (&v)[4][4]) {
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int64_t k = (int64_t)lane * 4 + 256 * m;
-    if (k < c.d) load4d(x + k, v[m]);
+    if (k < d) load4d(x + k, v[m]);
     else v[m][0] = v[m][1] = v[m][2] = v[m][3] = 0.0;
   }
+}
+
+// this lane's fma chains (before the wave sum): sum of squares / dot product in (m, c) order
+__device__ __forceinline__ double lane_sumsq(const double (&v)[4][4], int64_t d, int lane) {
   double ss = 0.0;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
-    if ((int64_t)lane * 4 + 256 * m < c.d)
+    if ((int64_t)lane * 4 + 256 * m < d)
 #pragma unroll
       for (int q = 0; q < 4; ++q) ss = fma(v[m][q], v[m][q], ss);
-  const double inv = row_inv_norm(wave_sum(ss), A.eps, A.flags);
+  return ss;
+}
+__device__ __forceinline__ double lane_dot(const double (&v)[4][4], const double (&w)[4][4], int64_t d, int lane) {
+  double dot = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if ((int64_t)lane * 4 + 256 * m < d)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dot = fma(v[m][q], w[m][q], dot);
+  return dot;
+}
+
+// pack row `row` of side A (held in v) into its planes with 1/||x|| = inv; lane 0 stores inv and the
+// bounds; eb = the row's bounds (lane 0)
+__device__ __forceinline__ void pack_regs(const EvalSide& A, const EvalCommon& c, int64_t row,
+                                          const double (&v)[4][4], double inv, int lane, float (&eb)[3]) {
+  uint16_t* hrow = A.hi + row * c.d_pad;
+  uint16_t* lrow = A.lo ? A.lo + row * c.d_pad : nullptr;
+  uint16_t* frow = A.h16 ? A.h16 + row * c.d_pad : nullptr;
   const bool want_f16 = frow != nullptr;
   PackAcc acc;
   if (c.mode == CMVE_SIM_F16 && want_f16) {
@@ -114,6 +120,20 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
     A.err_hilo[row] = eb[1];
     if (A.err_h16) A.err_h16[row] = eb[2];
   }
+}
+
+template <typename TA, typename TB>
+__device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide& B, const EvalCommon& c, int64_t row,
+                                              const TA* __restrict__ x, int lane, float (&eb)[3]) {
+  // the first GT partner's row is loaded beside the row itself (its index is known up front): the
+  // GT score then needs no second HBM round trip after the pack
+  const int64_t g_beg = A.off ? A.off[row] : 0, g_end = A.off ? A.off[row + 1] : 0;
+  double w0[4][4];
+  if (g_beg < g_end) load_row_regs((const TB*)B.raw + (int64_t)A.idx[g_beg] * B.ld, c.d, lane, w0);
+  double v[4][4];
+  load_row_regs(x, c.d, lane, v);
+  const double inv = row_inv_norm(wave_sum(lane_sumsq(v, c.d, lane)), A.eps, A.flags);
+  pack_regs(A, c, row, v, inv, lane, eb);
   if (!A.off) return;
   double best = -INFINITY;
   bool any = false;
@@ -125,24 +145,10 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
 #pragma unroll
         for (int q = 0; q < 4; ++q) w[m][q] = w0[m][q];
     } else {
-      const TB* y = (const TB*)B.raw + (int64_t)A.idx[g] * B.ld;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int64_t k = (int64_t)lane * 4 + 256 * m;
-        if (k < c.d) load4d(y + k, w[m]);
-      }
+      load_row_regs((const TB*)B.raw + (int64_t)A.idx[g] * B.ld, c.d, lane, w);
     }
-    double dot = 0.0, yy = 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if ((int64_t)lane * 4 + 256 * m < c.d)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dot = fma(v[m][q], w[m][q], dot);
-          yy = fma(w[m][q], w[m][q], yy);
-        }
-    const double invb = row_inv_norm(wave_sum(yy), B.eps, B.flags);
-    const double s = wave_sum(dot) * (inv * invb);  // wave_cos64(x, y, inv, invb)
+    const double invb = row_inv_norm(wave_sum(lane_sumsq(w, c.d, lane)), B.eps, B.flags);
+    const double s = wave_sum(lane_dot(v, w, c.d, lane)) * (inv * invb);  // wave_cos64(x, y, inv, invb)
     if (s == s) {
       any = true;
       if (s > best) best = s;
@@ -177,7 +183,7 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   }
   const TA* x = (const TA*)A.raw + row * A.ld;
   if (A.vec && B.vec && c.d_pad <= 1024) {
-    prep_row_regs<TA, TB>(A, B, c, row, x, hrow, lrow, frow, lane, eb);
+    prep_row_regs<TA, TB>(A, B, c, row, x, lane, eb);
     return;
   }
   const double inv = row_inv_norm(row_sumsq<TA>(x, c.d, A.vec != 0, lane), A.eps, A.flags);
@@ -287,6 +293,77 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide
   EVAL_STAMP(c, 0, 1);
 }
 
+// The prep of a one-to-one GT pairing (cmve_eval_ranks with CMVE_EVAL_PAIRED: caption i's only GT is
+// video p = q.idx[q.off[i]] and video p's only GT is caption i -- MSR-VTT-1kA's structure): ONE wave per
+// (caption, video) pair loads both rows once, packs both and scores the pair once for both directions.
+// Half the waves and half the row reads of eval_prep_kernel (which loads every row twice: as a row and as
+// its partner's GT), and the same bits: each side's norm, planes and bounds come from the same register
+// code, and the GT score fma(v, w) chain is symmetric in the two rows.  Padding rows i >= n of both sides
+// are this wave's too (q.n == g.n, q.n_pad == g.n_pad).
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  EVAL_STAMP(c, 0, 0);
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
+    c.bucket[t] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 10) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+  float ebq[3] = {0.f, 0.f, 0.f}, ebg[3] = {0.f, 0.f, 0.f};
+  if (i < q.n_pad && !(c.dbg & 1)) {
+    if (i >= q.n) {  // padding rows of both sides: zero vectors, zero bounds, never counted
+      const EvalSide* sides[2] = {&q, &g};
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        const EvalSide& A = *sides[sd];
+        pack_pad_row(A.hi + i * c.d_pad, A.lo ? A.lo + i * c.d_pad : nullptr, A.h16 ? A.h16 + i * c.d_pad : nullptr,
+                     c.d_pad, lane);
+        if (lane == 0) {
+          A.inv[i] = 0.0;
+          A.err_hi[i] = 0.f;
+          A.err_hilo[i] = 0.f;
+          if (A.err_h16) A.err_h16[i] = 0.f;
+          A.sgt[i] = (double)NAN;
+          A.cnt[i] = 0;
+        }
+      }
+    } else {
+      const int64_t p = q.idx[q.off[i]];
+      double v[4][4], w[4][4];
+      load_row_regs((const TQ*)q.raw + i * q.ld, c.d, lane, v);
+      load_row_regs((const TG*)g.raw + p * g.ld, c.d, lane, w);
+      const double ssq = wave_sum(lane_sumsq(v, c.d, lane)), ssg = wave_sum(lane_sumsq(w, c.d, lane));
+      const double invq = row_inv_norm(ssq, q.eps, q.flags), invg = row_inv_norm(ssg, g.eps, g.flags);
+      pack_regs(q, c, i, v, invq, lane, ebq);
+      pack_regs(g, c, p, w, invg, lane, ebg);
+      const double s = wave_sum(lane_dot(v, w, c.d, lane)) * (invq * invg);
+      if (lane == 0) {  // a one-entry list: its score, or +inf when it is NaN (prep_row_regs' encoding)
+        q.sgt[i] = s == s ? s : (double)INFINITY;
+        g.sgt[p] = s == s ? s : (double)INFINITY;
+        q.cnt[i] = 0;
+        g.cnt[p] = 0;
+      }
+    }
+  }
+  // err_max shards of both sides (eval_prep_kernel's scheme)
+  __shared__ float s_eb[PREP_NW][6];
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      s_eb[threadIdx.x >> 6][k] = ebq[k];
+      s_eb[threadIdx.x >> 6][3 + k] = ebg[k];
+    }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float m = 0.f;
+#pragma unroll
+    for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
+    unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];  // [side][plane] = tid
+    if (m == INFINITY) *sh = __float_as_uint(m);
+    else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
+  }
+  EVAL_STAMP(c, 0, 1);
+}
+
 constexpr int FIX_NT = 256;
 #ifndef CMVE_FIX_BLOCKS
 #define CMVE_FIX_BLOCKS 1024
@@ -382,22 +459,27 @@ template <typename TQ, typename TG>
 static int launch_eval_typed(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int phase, hipStream_t s) {
   if (phase == 0) {
     const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
-    hipLaunchKernelGGL((eval_prep_kernel<TQ, TG>), dim3(blocks), dim3(PREP_NT), 0, s, q, g, c);
+    cmve::launch(eval_prep_kernel<TQ, TG>, dim3(blocks), dim3(PREP_NT), 0u, s, q, g, c);
     return check_launch("eval_prep_kernel");
+  }
+  if (phase == 3) {  // the paired prep (eval_prep_pair_kernel): one wave per (caption, video) pair
+    const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);
+    cmve::launch(eval_prep_pair_kernel<TQ, TG>, dim3(blocks), dim3(PREP_NT), 0u, s, q, g, c);
+    return check_launch("eval_prep_pair_kernel");
   }
   if (phase == 1) {
     // 1,024 blocks of 4 waves, every wave one or two of the few thousand undecided pairs of an evaluation
     // of this size, in one flat walk (the rank fix-up's grid is sized for millions of pairs)
-    hipLaunchKernelGGL((eval_fix_kernel<TQ, TG>), dim3((unsigned)CMVE_FIX_BLOCKS), dim3(FIX_NT), 0, s, q, g, c);
+    cmve::launch(eval_fix_kernel<TQ, TG>, dim3((unsigned)CMVE_FIX_BLOCKS), dim3(FIX_NT), 0u, s, q, g, c);
     return check_launch("eval_fix_kernel");
   }
   const int64_t nmax = q.n > g.n ? q.n : g.n;
-  hipLaunchKernelGGL((eval_finish_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2), dim3(FIN_NT), 0,
-                     s, q, g, c);
+  cmve::launch(eval_finish_kernel<TQ, TG>, dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2), dim3(FIN_NT), 0u, s,
+               q, g, c);
   return check_launch("eval_finish_kernel");
 }
 
-// phase 0: prep, phase 1: fix-up, phase 2: err_max + ranks + R@K
+// phase 0: prep, phase 1: fix-up, phase 2: err_max + ranks + R@K, phase 3: the paired prep
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s) {
   if (!q_f64 && !g_f64) return launch_eval_typed<float, float>(q, g, c, phase, s);

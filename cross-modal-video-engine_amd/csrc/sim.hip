@@ -1073,7 +1073,7 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
     const int cus = std::max(8, device_cus() / 8 * 8);
     nblocks = std::min<unsigned>(nblocks, (unsigned)cus);
   }
-  hipLaunchKernelGGL((sim_kernel<MODE, EPI, WM, WN, TM, PHASED>), dim3(nblocks), dim3(G::NT), lds, stream, a);
+  cmve::launch(sim_kernel<MODE, EPI, WM, WN, TM, PHASED>, dim3(nblocks), dim3(G::NT), (uint32_t)lds, stream, a);
   return check_launch("sim_kernel");
 }
 
@@ -1529,10 +1529,14 @@ __global__ __launch_bounds__(256) void eval_thr_kernel(EvalThrSide s0, EvalThrSi
   s.lo[r] = sgt < INFINITY ? f32_round_down(sgt - E) : INFINITY;
 }
 
-extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode, const int64_t* row_off,
-                               const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx, void* ws,
-                               int64_t ws_bytes, int64_t cand_cap, int64_t* out, int32_t timing_slot) {
+extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags,
+                               const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
+                               const int32_t* col_idx, void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out,
+                               int32_t timing_slot) {
   CMVE_REQUIRE(h, "cmve_eval_ranks: NULL handle");
+  const int32_t mode = mode_flags & 0xff;
+  const bool paired_req = (mode_flags & CMVE_EVAL_PAIRED) != 0;
+  CMVE_REQUIRE((mode_flags & ~(0xff | CMVE_EVAL_PAIRED)) == 0, "cmve_eval_ranks: unknown flags 0x%x", mode_flags);
   int st = validate_pair(q, g, mode, "cmve_eval_ranks");
   if (st) return st;
   CMVE_REQUIRE(q->n > 0 && g->n > 0, "cmve_eval_ranks: both sets need rows");
@@ -1569,11 +1573,18 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "cmve_eval_ranks: gallery set too large (%lld buckets)",
                (long long)l.nb);
   hipEvent_t* ev = nullptr;
+  hipEvent_t* kev = nullptr;
   if (timing_slot >= 0) {
     ev = h->eval_ev[timing_slot];
     for (int k = 0; k < 4; ++k)
       if (!ev[k]) CMVE_HIP(hipEventCreate(&ev[k]));
+    kev = h->eval_kev[timing_slot];
+    for (int k = 0; k < 8; ++k)
+      if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
   }
+  auto arm = [&](int k) {  // the next launch's own start / stop (cmve::launch)
+    if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
+  };
   char* base = (char*)ws;
   cmve::EvalSide sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, out + CMVE_EVAL_OUT_HEAD);
   cmve::EvalSide sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt,
@@ -1602,9 +1613,15 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   c.stamps = (dbg & 128) ? stamp_buf : nullptr;
   g_eval_stamps = c.stamps;
   const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
+  if (paired_req)
+    CMVE_REQUIRE(row_off && col_off && q->n == g->n && q->n_pad == g->n_pad,
+                 "cmve_eval_ranks: CMVE_EVAL_PAIRED needs both directions and equal set sizes");
+  // the paired prep reads rows through the register path only (16-B pieces, d_pad <= 1024)
+  const bool paired = paired_req && sq.vec && sg.vec && q->d_pad <= 1024;
   hipStream_t s = h->stream;
   if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
-  st = cmve::launch_eval(sq, sg, c, qf, gf, 0, s);
+  arm(0);
+  st = cmve::launch_eval(sq, sg, c, qf, gf, paired ? 3 : 0, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
   SimArgs a = make_args(q, g, mode);
@@ -1643,11 +1660,14 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     st = check_launch("eval_thr_kernel");
     if (st) return st;
   }
+  arm(1);
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
+  arm(2);
   st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
   if (st) return st;
+  arm(3);
   st = cmve::launch_eval(sq, sg, c, qf, gf, 2, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
@@ -1669,7 +1689,8 @@ extern "C" int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows
   CMVE_REQUIRE(h && graph, "cmve_eval_graph_create: NULL handle / output");
   *graph = nullptr;
   CMVE_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-  const int st = cmve_eval_ranks(h, q, g, mode, row_off, row_idx, col_off, col_idx, ws, ws_bytes, cand_cap, out, -1);
+  const int st = cmve_eval_ranks(h, q, g, mode, row_off, row_idx, col_off, col_idx, ws, ws_bytes, cand_cap, out,
+                                 -1);  // (mode may carry CMVE_EVAL_PAIRED)
   hipGraph_t gr = nullptr;
   const hipError_t e = hipStreamEndCapture(h->stream, &gr);
   if (st) {  // (the argument check failed inside the capture: nothing was enqueued)
@@ -1709,5 +1730,14 @@ extern "C" int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3) {
   CMVE_REQUIRE(ev[0] && ev[3], "cmve_eval_timing: slot %d never recorded", slot);
   CMVE_HIP(hipEventSynchronize(ev[3]));
   for (int k = 0; k < 3; ++k) CMVE_HIP(hipEventElapsedTime(&ms3[k], ev[k], ev[k + 1]));
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4) {
+  CMVE_REQUIRE(h && ms4 && slot >= 0 && slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_kernel_timing: bad argument");
+  hipEvent_t* kev = h->eval_kev[slot];
+  CMVE_REQUIRE(kev[0] && kev[7], "cmve_eval_kernel_timing: slot %d never recorded", slot);
+  CMVE_HIP(hipEventSynchronize(kev[7]));
+  for (int k = 0; k < 4; ++k) CMVE_HIP(hipEventElapsedTime(&ms4[k], kev[2 * k], kev[2 * k + 1]));
   return CMVE_OK;
 }

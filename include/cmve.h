@@ -359,7 +359,7 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
                   int64_t* ranks, int64_t* recall);
 
 /*
- * K14 -- one exact two-direction GT-rank evaluation of a resident problem in THREE launches
+ * K14 -- one exact two-direction GT-rank evaluation of a resident problem in FOUR launches
  * (the reference's per-validation chain LINAS-engine/validate.py:61-74 / tester.py:133-139:
  * evaluation.cal_error (evaluation.py:17-21) then util/metrics.eval_q2m t2v and v2t (metrics.py:124-157)).
  *   launch 1: pack q and g from their raw rows (as cmve_pack_rows), exact fp64 GT scores of both
@@ -376,9 +376,14 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
  * for v2t; out[8] undecided pairs; out[9] 0, or the cand_cap a retry needs (a bucket overflowed: the
  * ranks are incomplete); out[16 ..] t2v ranks, then v2t ranks (1-based; cmve_gt_ranks' rules).
  * timing_slot in [0, CMVE_EVAL_TIMING_SLOTS) records handle events around the launches
- * (cmve_eval_timing reads them); -1 records none.
+ * (cmve_eval_timing reads them) and each launch's own start / stop (cmve_eval_kernel_timing); -1 records none.
+ * mode may carry CMVE_EVAL_PAIRED: the caller asserts a one-to-one GT pairing -- every t2v list is one
+ * video p = row_idx[row_off[i]], every v2t list is one caption, and v2t(p) = [i] (MSR-VTT-1kA's
+ * structure; q->n == g->n) -- and launch 1 then packs and scores each (caption, video) pair in one wave
+ * (half the row reads; same results bit for bit).  Lists that are not such a pairing give undefined ranks.
  */
 #define CMVE_EVAL_TIMING_SLOTS 32
+#define CMVE_EVAL_PAIRED 0x100
 #define CMVE_EVAL_OUT_HEAD 16
 int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int64_t* bytes);
 int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
@@ -387,6 +392,10 @@ int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mod
 /* Durations (ms) of the pack launch, the rank GEMM and the fix-up + ranks launches of the
  * cmve_eval_ranks call that used `slot` (waits for its last event). */
 int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3);
+/* the same evaluation's four kernel durations (ms4: prep, rank GEMM, fix-up, finish), each from its own
+ * launch's start / stop (hipExtLaunchKernelGGL: the dispatch timestamps rocprofv3 reports, without the
+ * dispatch gaps that events recorded between launches include); synchronises on the slot */
+int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
 /* Graph form of cmve_eval_ranks for an evaluation repeated on fixed buffers (the reference re-runs
  * validate.py:61-74 on new embeddings written into the same encode_* buffers; the bench's pipelined
  * steps): create captures the launches of one cmve_eval_ranks call (same arguments, no timing) on h's

@@ -650,3 +650,40 @@ def test_rank_session_stream_waits_for_the_producer(torch_cuda):
         t2v, _ = sess.run(q_t, g_t)     # no torch.cuda.synchronize() in between
         assert np.array_equal(t2v, exp), rep
 
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_paired_prep_equals_general_prep(torch_cuda, dt):
+    """CMVE_EVAL_PAIRED (one wave per (caption, video) pair, RankSession's choice for a one-to-one GT pairing
+    such as MSR-VTT-1kA) against the general prep on the same permuted pairing (padding rows, a zero video
+    whose caption's only GT scores NaN): identical ranks, R@K heads, packed planes, norms and bounds, and the
+    oracle's ranks."""
+    import torch
+    from cmve import engine
+    rng = np.random.default_rng(21)
+    n, d = 700, 384
+    perm = rng.permutation(n)
+    v = rng.standard_normal((n, d))
+    v[perm[3]] = 0.0  # caption 3's GT video is a zero row: its score is NaN (rank n)
+    c = v[perm] + 1.5 * rng.standard_normal((n, d))
+    t2v = [[int(perm[i])] for i in range(n)]
+    v2t = [[] for _ in range(n)]
+    for i in range(n):
+        v2t[int(perm[i])].append(i)
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    ct, vt = torch.from_numpy(c).to("cuda", tdt), torch.from_numpy(v).to("cuda", tdt)
+    sp = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=tdt)
+    sg = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=tdt)
+    assert sp.paired
+    sg.paired = False
+    r1, c1 = sp.run(ct, vt)
+    r2, c2 = sg.run(ct, vt)
+    assert np.array_equal(r1, r2) and np.array_equal(c1, c2)
+    assert sp.host[:10].tolist() == sg.host[:10].tolist()
+    for a, b in ((sp.q, sg.q), (sp.g, sg.g)):
+        for name in ("h16", "inv_norm", "err_h16"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), name
+    with np.errstate(invalid="ignore", divide="ignore"):
+        s = R.exact_scores64(ct.double().cpu().numpy(), vt.double().cpu().numpy())
+    assert np.array_equal(r1, R.rank_counts(s, t2v)) and np.array_equal(c1, R.rank_counts(s.T, v2t))
+    assert r1[3] == n

@@ -59,14 +59,16 @@ def main(outdir, tag):
         f, w = per[k]["FETCH_SIZE"], per[k]["WRITE_SIZE"]
         e = {"launches_traced": len(dur[k]),
              "trace_avg_ms": (sum(dur[k]) / len(dur[k])) if dur[k] else None,
+             "trace_total_ms": sum(dur[k]),
              "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
              "write_kib_per_launch": (sum(w) / len(w)) if w else None}
         if f and w:
             e["hbm_bytes_per_launch"] = 2 * e["fetch_kib_per_launch"] * 1024 + e["write_kib_per_launch"] * 1024
         kernels[k] = e
+    dominant = max(ROLES, key=lambda k: kernels[k]["trace_total_ms"])
     out = {"tag": tag, "workload": "MSR-VTT-1kA exact evaluation, 1000 x 1000 x 1024, float64 inputs",
-           "kernels": kernels,
-           "hbm_bytes_per_launch": kernels["rank_gemm"].get("hbm_bytes_per_launch"),
+           "kernels": kernels, "dominant": dominant,
+           "hbm_bytes_per_launch": kernels[dominant].get("hbm_bytes_per_launch"),
            "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"}
     json.dump(out, open(os.path.join(prof, f"{tag}_1ka_traffic.json"), "w"), indent=1)
     print(json.dumps(out))
