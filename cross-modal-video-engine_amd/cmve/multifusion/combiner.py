@@ -90,6 +90,8 @@ class Combiner(nn.Module):
         self.dropout6 = nn.Dropout(0.5)
         self.dropout7 = nn.Dropout(0.5)
         self._pk = {}
+        # K9b absorbed attention (fusion.hip); False = the projected-K/V path (cmve_mha_1q), kept for A/B and tests
+        self.absorbed = True
         self._cat_key = None
         self._cat_w = self._cat_b = None
 
@@ -105,6 +107,44 @@ class Combiner(nn.Module):
             self._cat_b = torch.cat([a.bias.detach(), b.bias.detach()], 0).float().contiguous()
             self._cat_key = key
         return self._cat_w, self._cat_b
+
+    def _absorbed(self, npix: int):
+        """The attention's K / V in-projections absorbed (fusion.hip K9b, combiner.py:38-40): per head h
+        (dh = d / H, gamma / beta = ln_1's affine, perm = the kernel's element order within a key run,
+        e = p * (d / npix) + c' <-> original c' * npix + p):
+          M[h d + e, :] = gamma_j / sqrt(dh) * (W_k,h^T W_q,h)[j, :],  c[h d + e] = gamma_j / sqrt(dh) * (W_k,h^T b_q,h)_j
+          N[:, h d + e] = (W_o,h W_v,h)[:, j] * gamma_j,               bN = W_o (W_v beta + b_v) + b_o
+        with j = perm[e]: scores u_h . n_t equal q'_h . K_t,h / sqrt(dh) up to terms constant over the keys, and
+        z @ N^T + bN equals out_proj(concat_h sum_t p_t V_t,h).  Formed in fp64, stored fp32, cached per weight
+        version."""
+        blk = self.self_attn_1
+        W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
+        Wo, bo = blk.attn.out_proj.weight, blk.attn.out_proj.bias
+        g, be = blk.ln_1.weight, blk.ln_1.bias
+        key = tuple((t.data_ptr(), t._version) for t in (W, Bi, Wo, bo, g, be)) + (npix,)
+        if getattr(self, "_abs_key", None) != key:
+            d, H = W.shape[1], self.nhead
+            dh, cpr = d // H, d // npix
+            Wd, bd = W.detach().double(), Bi.detach().double()
+            Wq, Wk, Wv = Wd[:d], Wd[d:2 * d], Wd[2 * d:]
+            bq, bv = bd[:d], bd[2 * d:]
+            Wod, bod = Wo.detach().double(), bo.detach().double()
+            gd, bed = g.detach().double(), be.detach().double()
+            p, c = torch.meshgrid(torch.arange(npix), torch.arange(cpr), indexing="ij")
+            perm = (c * npix + p).reshape(-1).to(W.device)
+            sc = 1.0 / (dh ** 0.5)
+            Ms, cs, Ns = [], [], []
+            for h in range(H):
+                sl = slice(h * dh, (h + 1) * dh)
+                Ms.append(((Wk[sl].t() @ Wq[sl]) * (gd * sc)[:, None])[perm])
+                cs.append(((Wk[sl].t() @ bq[sl]) * gd * sc)[perm])
+                Ns.append(((Wod[:, sl] @ Wv[sl]) * gd[None, :])[:, perm])
+            self._abs_M = torch.cat(Ms, 0).float().contiguous()
+            self._abs_c = torch.cat(cs, 0).float().contiguous()
+            self._abs_N = torch.cat(Ns, 1).float().contiguous()
+            self._abs_bN = (Wod @ (Wv @ bed + bv) + bod).float().contiguous()
+            self._abs_key = key
+        return self._abs_M, self._abs_c, self._abs_N, self._abs_bN
 
     def time_process(self, fea):
         """combiner.py:140-143: mean over the frame axis."""
@@ -157,18 +197,32 @@ class Combiner(nn.Module):
         # reshape(l*f, b, d); with G batches of gs rows each batch's raw reshape is taken separately and
         # interleaved, row t*b + g*gs + bb -- written in that order straight from the conv output
         blk = self.self_attn_1
-        kv_in = engine.transpose_blocks_kv(y, 16, y.shape[1], d, l * f, gs, b)
-        kv_ln = engine.PackedOperand.layernorm(kv_in, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps)
         q_ln = _layernorm(p_r_m, blk.ln_1)
-        W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
-        q = _linear(q_ln, W[:d], Bi[:d], packed=self._p("in_q"))
-        kv = _linear(kv_ln, W[d:], Bi[d:], packed=self._p("in_kv"))          # [l*f*b, 2d]: K | V
-        attn = torch.empty((b, d), dtype=torch.float32, device=text.device)
-        check(lib.cmve_mha_1q(engine.handle(text.device), engine._ptr(q), q.stride(0), engine._ptr(kv), kv.stride(0), d,
-                              b, l * f, self.nhead, d // self.nhead, engine._ptr(attn), attn.stride(0)), "cmve_mha_1q")
-        v3 = kv_in.view(l * f, b, d)
-        v_mean = temporal_pool(v3.transpose(0, 1), "mean")                    # v.mean(dim=0), strided view
-        x = _linear(attn, blk.attn.out_proj.weight, blk.attn.out_proj.bias, resid=v_mean, packed=self._p("out_proj"))
+        if self.absorbed and d % 16 == 0 and (d, self.nhead) in ((640, 8), (512, 8)):
+            # K9b: K / V projections absorbed (see _absorbed); the keys are read straight from the conv output
+            M, cu, N, bN = self._absorbed(16)
+            u = _linear(q_ln, M, cu, packed=self._p("abs_m"))                # [b, H d]
+            z = torch.empty((b, self.nhead * d), dtype=torch.float32, device=text.device)
+            v_mean = torch.empty((b, d), dtype=torch.float32, device=text.device)
+            check(lib.cmve_mha_absorbed(engine.handle(text.device), engine._ptr(y), y.stride(0), y.shape[1], 16, f, gs,
+                                        b, self.nhead, d, engine._ptr(u), u.stride(0), float(blk.ln_1.eps),
+                                        engine._ptr(z), z.stride(0), engine._ptr(v_mean), v_mean.stride(0)),
+                  "cmve_mha_absorbed")
+            x = _linear(z, N, bN, resid=v_mean, packed=self._p("abs_n"))
+        else:
+            kv_in = engine.transpose_blocks_kv(y, 16, y.shape[1], d, l * f, gs, b)
+            kv_ln = engine.PackedOperand.layernorm(kv_in, blk.ln_1.weight, blk.ln_1.bias, blk.ln_1.eps)
+            W, Bi = blk.attn.in_proj_weight, blk.attn.in_proj_bias
+            q = _linear(q_ln, W[:d], Bi[:d], packed=self._p("in_q"))
+            kv = _linear(kv_ln, W[d:], Bi[d:], packed=self._p("in_kv"))          # [l*f*b, 2d]: K | V
+            attn = torch.empty((b, d), dtype=torch.float32, device=text.device)
+            check(lib.cmve_mha_1q(engine.handle(text.device), engine._ptr(q), q.stride(0), engine._ptr(kv),
+                                  kv.stride(0), d, b, l * f, self.nhead, d // self.nhead, engine._ptr(attn),
+                                  attn.stride(0)), "cmve_mha_1q")
+            v3 = kv_in.view(l * f, b, d)
+            v_mean = temporal_pool(v3.transpose(0, 1), "mean")                    # v.mean(dim=0), strided view
+            x = _linear(attn, blk.attn.out_proj.weight, blk.attn.out_proj.bias, resid=v_mean,
+                        packed=self._p("out_proj"))
         h = _linear(_layernorm(x, blk.ln_2), blk.mlp.c_fc.weight, blk.mlp.c_fc.bias, ACT_QUICKGELU,
                     packed=self._p("c_fc"))
         based = _linear(h, blk.mlp.c_proj.weight, blk.mlp.c_proj.bias, resid=x, packed=self._p("c_proj"))

@@ -251,6 +251,147 @@ __global__ __launch_bounds__(256) void mha_1q_rows_kernel(const float* __restric
     out[(int64_t)b * ldo + e] = (po[e] + po[D + e]) + (po[2 * D + e] + po[3 * D + e]);
 }
 
+// ---------------------------------------------------------------------------
+// K9b: the Combiner's attention with its K / V in-projections ABSORBED into the query and output
+// sides (combiner.py:38-40 with k = v = p_s_m.reshape(l*f, b, d), combiner.py:164-166).  Per head h,
+// with n_t = (x_t - mean_t) * rstd_t the un-affined LayerNorm of key row x_t:
+//   q'_h . K_t,h = n_t . (gamma (.) W_k,h^T q'_h) + (terms constant over t: softmax-invariant, dropped)
+//   sum_t p_t V_t,h = W_v,h (gamma (.) z_h + beta) + b_v,h,   z_h = sum_t p_t n_t
+// so the host folds W_k into the query GEMM (u_h = gamma (.) W_k,h^T (W_q,h ln(q) + b_q,h) / sqrt(dh), one
+// [d] -> [H d] GEMM) and W_v / out_proj into one [H d] -> [d] GEMM after this kernel, and the 128 key rows
+// of a query are never projected: 2 * 128 * d * 2d MACs per query become ~2 * H * d * d.  This kernel
+// reads the key rows STRAIGHT from the conv1x1 GEMM output y ([B f npix, C]: row (bf, p), column c = the
+// conv output at channel c, pixel p), whose raw reshape (combiner.py:159,164) makes key run r of block bf
+// the channels [r cpr, (r + 1) cpr) x all npix pixels (cpr = d / npix): no transpose, no LayerNorm pass,
+// no K / V matrix.  Kernel element order within a run: e = p * cpr + c'  (original element c' npix + p);
+// the host permutes the absorbed weights to match.  One wave per query, all H heads, online softmax
+// (running max / sum per head); v.mean(0) (combiner.py:40) from the same rows.  LayerNorm statistics in
+// fp32 two-pass (torch's fp32 LayerNorm subclass, combiner.py:11-17).
+__device__ __forceinline__ float wave_sum_f32(float v) {  // every lane gets the same bits
+  v = group_sum_f32(v, 16);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+template <int E, int HW, int NWV>  // HW heads per wave, NWV waves per block (one query): H = HW * NWV
+__global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __restrict__ y, int64_t ldy, int npix, int cpr,
+                                                          int L, int f, int gs, const float* __restrict__ u,
+                                                          int64_t ldu, float eps, float* __restrict__ z, int64_t ldz,
+                                                          float* __restrict__ vmean, int64_t ldv) {
+  constexpr int D = 64 * E, E2 = E / 2, H = HW;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // heads [wv HW, (wv + 1) HW)
+  const int64_t qb = blockIdx.x;
+  const int64_t g = qb / gs, bb = qb - g * gs;
+  const int T = f * L, cpr2 = cpr >> 1;
+  int64_t off[E2];  // this lane's float2 pieces of a key run: pixel p, channel pair c2
+#pragma unroll
+  for (int m = 0; m < E2; ++m) {
+    const int fi = lane + 64 * m, p = fi / cpr2, c2 = fi - p * cpr2;
+    off[m] = (int64_t)p * ldy + 2 * c2;
+  }
+  float uu[H][E];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int m = 0; m < E2; ++m) {
+      const float2 w = *(const float2*)(u + qb * ldu + (wv * HW + h) * D + 2 * (lane + 64 * m));
+      uu[h][2 * m] = w.x;
+      uu[h][2 * m + 1] = w.y;
+    }
+  auto row_base = [&](int t) {
+    const int64_t R = (int64_t)t * gs + bb;
+    const int64_t bf = g * gs * f + R / L;
+    return y + bf * npix * ldy + (R % L) * cpr;
+  };
+  float acc[H][E], mx[H], sm[H], vs[E];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    mx[h] = -INFINITY;
+    sm[h] = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[h][e] = 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) vs[e] = 0.f;
+  float2 nxt[E2];
+  {
+    const float* b0 = row_base(0);
+#pragma unroll
+    for (int m = 0; m < E2; ++m) nxt[m] = *(const float2*)(b0 + off[m]);
+  }
+  for (int t = 0; t < T; ++t) {
+    float x[E];
+#pragma unroll
+    for (int m = 0; m < E2; ++m) {
+      x[2 * m] = nxt[m].x;
+      x[2 * m + 1] = nxt[m].y;
+    }
+    if (t + 1 < T) {  // the next key row's loads in flight behind this row's arithmetic
+      const float* bn = row_base(t + 1);
+#pragma unroll
+      for (int m = 0; m < E2; ++m) nxt[m] = *(const float2*)(bn + off[m]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      s += x[e];
+      vs[e] += x[e];
+    }
+    const float mean = wave_sum_f32(s) / (float)D;
+    float c[E], q = 0.f, dot[H];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      c[e] = x[e] - mean;
+      q = fmaf(c[e], c[e], q);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float a = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) a = fmaf(c[e], uu[h][e], a);
+      dot[h] = a;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum_f32(q) / (float)D + eps);
+#pragma unroll
+    for (int e = 0; e < E; ++e) c[e] *= rstd;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float sc = wave_sum_f32(dot[h]) * rstd;  // wave-uniform
+      if (sc > mx[h]) {
+        const float k = expf(mx[h] - sc);  // 0 on the first row
+        sm[h] *= k;
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[h][e] *= k;
+        mx[h] = sc;
+      }
+      const float p = expf(sc - mx[h]);
+      sm[h] += p;
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, c[e], acc[h][e]);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float inv = 1.0f / sm[h];
+#pragma unroll
+    for (int m = 0; m < E2; ++m)
+      *(float2*)(z + qb * ldz + (wv * HW + h) * D + 2 * (lane + 64 * m)) =
+          make_float2(acc[h][2 * m] * inv, acc[h][2 * m + 1] * inv);
+  }
+  if (wv != 0) return;  // v.mean(0): wave 0's sums
+  const float invT = 1.0f / (float)T;
+#pragma unroll
+  for (int m = 0; m < E2; ++m) {
+    const int fi = lane + 64 * m, p = fi / cpr2, c0 = 2 * (fi - p * cpr2);
+    vmean[qb * ldv + (int64_t)c0 * npix + p] = vs[2 * m] * invT;
+    vmean[qb * ldv + (int64_t)(c0 + 1) * npix + p] = vs[2 * m + 1] * invT;
+  }
+}
+
 // out = normalize( ((y + ds*text) + (1-ds)*ref) + based , eps )
 __global__ __launch_bounds__(256) void fuse_combine_kernel(const float* __restrict__ y, const float* __restrict__ ds,
                                                            const float* __restrict__ text,
@@ -474,6 +615,33 @@ extern "C" int cmve_mha_1q(cmve_handle_t h, const float* q, int64_t ldq, const f
   hipLaunchKernelGGL(mha_1q_kernel, dim3((unsigned)B, (unsigned)H), dim3(256), lds, h->stream, q, ldq, kv, ldkv, v_off,
                      B, T, H, dh, out, ldo);
   return check_launch("mha_1q");
+}
+
+extern "C" int cmve_mha_absorbed(cmve_handle_t h, const float* y, int64_t ldy, int64_t C, int64_t npix, int64_t f,
+                                 int64_t gs, int64_t B, int32_t H, int64_t d, const float* u, int64_t ldu, double eps,
+                                 float* z, int64_t ldz, float* vmean, int64_t ldv) {
+  CMVE_REQUIRE(h && y && u && z && vmean, "cmve_mha_absorbed: NULL argument");
+  CMVE_REQUIRE(B >= 0 && f > 0 && gs > 0 && B % gs == 0 && npix > 0 && C > 0 && d > 0 && H > 0,
+               "cmve_mha_absorbed: bad shape (B a multiple of gs)");
+  CMVE_REQUIRE(d % npix == 0 && (d / npix) % 2 == 0 && C % (d / npix) == 0,
+               "cmve_mha_absorbed: d / npix channels per key run, even, dividing C");
+  CMVE_REQUIRE(ldy >= C && ldu >= H * d && ldz >= H * d && ldv >= d && ldy % 2 == 0 && ldu % 2 == 0 && ldz % 2 == 0 &&
+                   ((uintptr_t)y & 7) == 0 && ((uintptr_t)u & 7) == 0 && ((uintptr_t)z & 7) == 0,
+               "cmve_mha_absorbed: strides / 8-byte alignment");
+  if (B == 0) return CMVE_OK;
+  const int cpr = (int)(d / npix), L = (int)(C / cpr);
+  if (d == 640 && H == 8) {  // the Combiner: d 640 = 64 lanes x 10, 8 heads
+    hipLaunchKernelGGL((mha_absorbed_kernel<10, 4, 2>), dim3((unsigned)B), dim3(128), 0, h->stream, y, ldy, (int)npix, cpr,
+                       L, (int)f, (int)gs, u, ldu, (float)eps, z, ldz, vmean, ldv);
+    return check_launch("mha_absorbed");
+  }
+  if (d == 512 && H == 8) {
+    hipLaunchKernelGGL((mha_absorbed_kernel<8, 4, 2>), dim3((unsigned)B), dim3(128), 0, h->stream, y, ldy, (int)npix, cpr,
+                       L, (int)f, (int)gs, u, ldu, (float)eps, z, ldz, vmean, ldv);
+    return check_launch("mha_absorbed");
+  }
+  set_error("cmve_mha_absorbed: instantiated for (d, H) = (640, 8), (512, 8)");
+  return CMVE_E_UNSUPPORTED;
 }
 
 extern "C" int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* ds, const float* text, const float* ref,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 13
+#define CMVE_ABI_VERSION 14
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -192,6 +192,19 @@ int cmve_mha_1q(cmve_handle_t h, const float* q, int64_t ldq, const float* kv, i
                 int32_t B, int32_t T, int32_t H, int32_t dh, float* out, int64_t ldo);
 int cmve_fuse_combine(cmve_handle_t h, const float* y, const float* ds, const float* text, const float* ref,
                       const float* based, int64_t n, int64_t d, double eps, float* out);
+/* K9b: the same attention (combiner.py:38-40, k = v = p_s_m.reshape(l*f, b, d), combiner.py:159,164-166) with
+ * the K / V in-projections absorbed: the host folds W_k into the query side, u [B, H*d] (per head
+ * gamma (.) W_k,h^T q'_h / sqrt(dh), element order below), and W_v / out_proj into one GEMM after this call.
+ * The key rows are read straight from the conv1x1 GEMM output y [B*f*npix, C] (row (bf, p), column c): key
+ * t of query qb = g*gs + bb is run R % L of block bf = g*gs*f + R / L, R = t*gs + bb (cpr = d / npix channels
+ * per run, L = C / cpr runs per block, T = f*L keys) -- the raw reshapes of combiner.py:159,164-165 for
+ * B / gs consecutive batches of gs rows (gs = B: one batch).  Within a run, element e = p*cpr + c' is the
+ * original element c'*npix + p.  Out: z [B, H*d] = per head sum_t softmax_t(u_h . n_t) n_t (n_t the
+ * un-affined LayerNorm of key t, eps), in the kernel's element order; vmean [B, d] = v.mean(0) in the
+ * original order.  Instantiated for (d, H) = (640, 8) and (512, 8). */
+int cmve_mha_absorbed(cmve_handle_t h, const float* y, int64_t ldy, int64_t C, int64_t npix, int64_t f, int64_t gs,
+                      int64_t B, int32_t H, int64_t d, const float* u, int64_t ldu, double eps, float* z, int64_t ldz,
+                      float* vmean, int64_t ldv);
 /*
  * The raw reshapes around Combiner's conv1x1 (MultiFusion/src/combiner.py:159,164): block b of x is
  * [R][C] row-major and its column c becomes row (b, c) of the output.

@@ -29,13 +29,17 @@ def test_oracle_batch_mixing_and_logits(golden, state):
 
 
 @pytest.mark.gpu
-def test_gpu_combiner(golden, state):
+@pytest.mark.parametrize("absorbed", [True, False])
+def test_gpu_combiner(golden, state, absorbed):
+    """Both attention paths against the reference module's outputs: K9b (K / V projections absorbed, keys read
+    from the conv output, cmve_mha_absorbed) and the projected-K/V path (cmve_mha_1q)."""
     import torch
     from cmve.multifusion.combiner import Combiner
     g = golden("combiner")
     m = Combiner(640, 2560, 5120).cuda()
     m.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()})
     m.eval()
+    m.absorbed = absorbed
     for b, seed in ((32, 21), (7, 22), (1, 23)):
         high, mid, text, tgt = synth.combiner_inputs(b, seed)
         pred = m.combine_features((torch.from_numpy(high).cuda(), torch.from_numpy(mid).cuda()),
@@ -49,6 +53,31 @@ def test_gpu_combiner(golden, state):
     alone = m.combine_features((torch.from_numpy(high[:7]).cuda(), torch.from_numpy(mid[:7]).cuda()),
                                torch.from_numpy(text[:7]).cuda())
     np.testing.assert_allclose(alone.cpu().numpy(), g["pred_b32_first7_alone"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_absorbed_attention_matches_projected(state):
+    """K9b against the projected-K/V path on a C4-sized grouped batch (combine_batches, 8 batches of 32):
+    the same function up to fp32 rounding (unit rows: 2e-6 absolute), and the absorbed weights follow a
+    weight update (cache keyed on the parameters' versions)."""
+    import torch
+    from cmve.multifusion.combiner import Combiner
+    m = Combiner(640, 2560, 5120).cuda()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()})
+    m.eval()
+    parts = [synth.combiner_inputs(32, 50 + i)[:3] for i in range(8)]
+    high, mid, text = (torch.from_numpy(np.concatenate([p[j] for p in parts])).cuda() for j in range(3))
+    a = m.combine_batches((high, mid), text)
+    m.absorbed = False
+    p = m.combine_batches((high, mid), text)
+    assert (a - p).abs().max().item() < 2e-6
+    with torch.no_grad():
+        m.self_attn_1.attn.in_proj_weight.mul_(1.5)
+        m.self_attn_1.ln_1.weight.add_(0.25)
+    p2 = m.combine_batches((high, mid), text)
+    m.absorbed = True
+    a2 = m.combine_batches((high, mid), text)
+    assert (a2 - p2).abs().max().item() < 2e-6 and (a2 - a).abs().max().item() > 1e-4
 
 
 @pytest.mark.gpu

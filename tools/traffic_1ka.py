@@ -26,7 +26,7 @@ ROLES = ("pack_gt_scores", "rank_gemm", "fixup", "ranks_recall")
 
 
 def role(name):
-    if "eval_prep_kernel" in name:
+    if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name:
         return "pack_gt_scores"
     if "eval_fix_kernel" in name:
         return "fixup"
