@@ -157,6 +157,7 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
   if (lane == 0) {
     A.sgt[row] = any ? best : (g_end > g_beg ? (double)INFINITY : (double)NAN);
     A.cnt[row] = 0;
+    if (A.gt1) A.gt1[row] = g_end > g_beg ? A.idx[g_beg] : -1;
   }
 }
 
@@ -177,6 +178,7 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
       if (A.off) {
         A.sgt[row] = (double)NAN;
         A.cnt[row] = 0;
+        if (A.gt1) A.gt1[row] = -1;
       }
     }
     return;
@@ -215,6 +217,7 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
     // empty list: NaN (rank n_m + 1); every GT NaN: +inf (rank n_m) -- gt_thr_kernel's encoding
     A.sgt[row] = any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN);
     A.cnt[row] = 0;
+    if (A.gt1) A.gt1[row] = A.off[row + 1] > A.off[row] ? A.idx[A.off[row]] : -1;
   }
 }
 
@@ -324,6 +327,7 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, Eva
           if (A.err_h16) A.err_h16[i] = 0.f;
           A.sgt[i] = (double)NAN;
           A.cnt[i] = 0;
+          if (A.gt1) A.gt1[i] = -1;
         }
       }
     } else {
@@ -341,6 +345,8 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, Eva
         g.sgt[p] = s == s ? s : (double)INFINITY;
         q.cnt[i] = 0;
         g.cnt[p] = 0;
+        if (q.gt1) q.gt1[i] = (int32_t)p;
+        if (g.gt1) g.gt1[p] = (int32_t)i;
       }
     }
   }

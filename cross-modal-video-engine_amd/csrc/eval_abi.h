@@ -30,6 +30,8 @@ struct EvalSide {
   float* thr_lo;
   int32_t* cnt;
   int64_t* ranks;      // out: 1-based ranks of this direction
+  int32_t* gt1;        // the first GT of each row (idx[off[row]], -1: none / padding), written by the prep: the
+                       // rank GEMM drops that GT pair from the undecided list (it can never be counted)
 };
 
 struct EvalCommon {

@@ -84,6 +84,10 @@ struct SimArgs {
   // 256 gallery rows: a 1k x 1k evaluation otherwise sends every wave's slot reservation to one of 4 counters
   int tile_buckets;
   int nbn64;
+  // K14: the first GT of every row / column (-1: none); the 2-stage / ring rank epilogues drop that GT pair
+  // from the undecided list -- a GT item's score never exceeds its row's best GT score, so it is never counted
+  const int* row_gt1;
+  const int* col_gt1;
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
@@ -386,6 +390,31 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // K14 (2-stage / ring rank kernels): the first GT of this lane's rows (i, r) and columns (j), fetched with
+  // the thresholds; the epilogue clears those GT pairs' band bits (a GT pair is never counted: 1,000 of a
+  // 1k-A evaluation's ~1,300 undecided t2v pairs are the GT pairs themselves)
+  constexpr bool GT_SKIP = !PHASED && EPI == EPI_RANK;
+  int gt_row[GT_SKIP ? TM : 1][4], gt_col[GT_SKIP ? TN : 1];
+#pragma unroll
+  for (int i = 0; i < (GT_SKIP ? TM : 1); ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gt_row[i][r] = -1;
+#pragma unroll
+  for (int j = 0; j < (GT_SKIP ? TN : 1); ++j) gt_col[j] = -1;
+  auto fetch_gt1 = [&]() {
+    if constexpr (GT_SKIP) {
+      const int rb = m0 + wr * (TM * 16) + (lane >> 4) * 4, cb = n0 + wc * (TN * 16) + (lane & 15);
+      if (a.row_gt1)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gt_row[i][r] = a.row_gt1[rb + i * 16 + r];  // (n_pad entries)
+      if (a.col_gt1)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) gt_col[j] = a.col_gt1[cb + j * 16];
+    }
+  };
+
   auto epilogue = [&]() {
   #ifdef CMVE_DBG_NOEPI  // diagnostic build only: main loop without any epilogue (results are garbage)
   #pragma unroll
@@ -621,6 +650,23 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         fast_block(std::true_type{}, std::false_type{});
       } else {
         fast_block(std::false_type{}, std::true_type{});
+      }
+      if constexpr (GT_SKIP) {  // drop the GT pairs (row band: column = the row's GT; column band: row = the column's)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          uint32_t m = 0u;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int dc = gt_row[i][r] - cbase;
+            m |= (dc >= 0 && dc < TN * 16 && (dc & 15) == 0) ? 1u << ((dc >> 4) * 4 + r) : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int dr = gt_col[j] - (rbase + i * 16);
+            m |= (dr >= 0 && dr < 4) ? 1u << (16 + j * 4 + dr) : 0u;
+          }
+          und[i] &= ~m;
+        }
       }
       cc_pack += __shfl_xor(cc_pack, 16, 64);
       cc_pack += __shfl_xor(cc_pack, 32, 64);
@@ -898,6 +944,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
         sgt_raw = tid < BM ? a.row_sgt[m0 + tid] : a.col_sgt[n0 + tid - BM];
         e_raw = tid < BM ? a.q_err[m0 + tid] : a.g_err[n0 + tid - BM];
       }
+      fetch_gt1();
     }
   }
   CMVE_STAMP(1);
@@ -975,6 +1022,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
     if (a.thr_gt) {  // overlaps the first K-tile's loads
       reduce_err_max();
       fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
+      fetch_gt1();
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1427,7 +1475,7 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
 
 namespace {
 struct EvalWs {
-  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, cand, total;
+  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, q_gt1, g_gt1, cand, total;
 };
 EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1450,6 +1498,10 @@ EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
   w.g_lo = o;
   o = up(o + 4 * (size_t)ng_pad);
   w.g_cnt = o;
+  o = up(o + 4 * (size_t)ng_pad);
+  w.q_gt1 = o;
+  o = up(o + 4 * (size_t)nq_pad);
+  w.g_gt1 = o;
   o = up(o + 4 * (size_t)ng_pad);
   w.cand = o;
   o = up(o + 8 * (size_t)cand_cap);
@@ -1476,7 +1528,7 @@ extern "C" int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, i
 }
 
 static cmve::EvalSide eval_side(cmve_rows_t* r, const int64_t* off, const int32_t* idx, char* ws, size_t o_sgt,
-                                size_t o_hi, size_t o_lo, size_t o_cnt, int64_t* ranks) {
+                                size_t o_hi, size_t o_lo, size_t o_cnt, size_t o_gt1, int64_t* ranks) {
   cmve::EvalSide s{};
   s.raw = r->raw;
   s.ld = r->raw_ld;
@@ -1500,6 +1552,7 @@ static cmve::EvalSide eval_side(cmve_rows_t* r, const int64_t* off, const int32_
   s.thr_hi = (float*)(ws + o_hi);
   s.thr_lo = (float*)(ws + o_lo);
   s.cnt = (int32_t*)(ws + o_cnt);
+  s.gt1 = off ? (int32_t*)(ws + o_gt1) : nullptr;
   s.ranks = ranks;
   return s;
 }
@@ -1586,8 +1639,9 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
   };
   char* base = (char*)ws;
-  cmve::EvalSide sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, out + CMVE_EVAL_OUT_HEAD);
-  cmve::EvalSide sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt,
+  cmve::EvalSide sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, w.q_gt1,
+                                out + CMVE_EVAL_OUT_HEAD);
+  cmve::EvalSide sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt, w.g_gt1,
                                 out + CMVE_EVAL_OUT_HEAD + q->n);
   cmve::EvalCommon c{};
   c.d = q->d;
@@ -1650,6 +1704,10 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   a.cap_b = l.cap_b;
   a.tile_buckets = tile_buckets;
   a.nbn64 = (int)(g->n_pad >> 6);
+  if (a.thr_gt) {  // (the 2-stage / ring kernels; the persistent G256 kernel keeps every undecided pair)
+    a.row_gt1 = sq.gt1;
+    a.col_gt1 = sg.gt1;
+  }
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
   if (!a.thr_gt) {
     EvalThrSide t0{a.row_sgt, a.q_err, a.g_emax, row_off ? sq.thr_hi : nullptr, sq.thr_lo, q->n_pad};
