@@ -174,6 +174,56 @@ __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB*
   return wave_sum(acc);
 }
 
+// wave_dot64 of two pairs at once: every load of both pairs in flight before either fma chain, each
+// chain in wave_dot64's own order (the same bits as two wave_dot64 calls); unaligned pairs take those calls
+template <typename TA, typename TB>
+__device__ __forceinline__ void wave_dot64_x2(const TA* __restrict__ a, const TB* __restrict__ b,
+                                              const TA* __restrict__ a2, const TB* __restrict__ b2, int64_t d,
+                                              int lane, double& s1, double& s2) {
+  if ((d & 3) == 0 && ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)a2) | ((uintptr_t)b2)) & 15) == 0) {
+    double acc = 0.0, acc2 = 0.0;
+    auto fma4 = [](double& s, const double (&x)[4], const double (&y)[4]) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s = fma(x[c], y[c], s);
+    };
+    int64_t k = (int64_t)lane * 4;
+    for (; k + 768 < d; k += 1024) {
+      double x[4][4], y[4][4], x2[4][4], y2[4][4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        load4d(a + k + 256 * m, x[m]);
+        load4d(b + k + 256 * m, y[m]);
+        load4d(a2 + k + 256 * m, x2[m]);
+        load4d(b2 + k + 256 * m, y2[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        fma4(acc, x[m], y[m]);
+        fma4(acc2, x2[m], y2[m]);
+      }
+    }
+    for (; k < d; k += 256) {
+      double x[4], y[4], x2[4], y2[4];
+      load4d(a + k, x);
+      load4d(b + k, y);
+      load4d(a2 + k, x2);
+      load4d(b2 + k, y2);
+      fma4(acc, x, y);
+      fma4(acc2, x2, y2);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // wave_sum of both, interleaved
+      acc += __shfl_xor(acc, o, 64);
+      acc2 += __shfl_xor(acc2, o, 64);
+    }
+    s1 = acc;
+    s2 = acc2;
+    return;
+  }
+  s1 = wave_dot64(a, b, d, lane);
+  s2 = wave_dot64(a2, b2, d, lane);
+}
+
 // fp64 -> fp32 with directed rounding
 __device__ __forceinline__ float f32_round_up(double x) {
   float f = (float)x;

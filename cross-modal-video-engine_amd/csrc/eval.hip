@@ -398,7 +398,7 @@ __device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
   block_reduce_k<true>(mx, redm);
   if (threadIdx.x == 0) {
     c.stats[8] = (int64_t)tot[0];
-    c.stats[9] = (int64_t)mx[0] > c.cap_b ? ((int64_t)mx[0] + 1) * c.nb + c.nb + 1 : 0;
+    c.stats[9] = (!c.fix_inline && (int64_t)mx[0] > c.cap_b) ? ((int64_t)mx[0] + 1) * c.nb + c.nb + 1 : 0;
   }
 }
 

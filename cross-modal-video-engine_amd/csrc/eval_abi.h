@@ -43,6 +43,7 @@ struct EvalCommon {
   int64_t nb, cap_b;
   const uint64_t* cand;
   int64_t* stats;              // out[0, 16)
+  int fix_inline;              // the rank GEMM re-scored the undecided pairs itself (no list: never an overflow)
   int dbg;                     // kernel studies only (CMVE_EVAL_DBG): skip parts, results garbage
   unsigned long long* stamps;  // kernel studies only (CMVE_EVAL_DBG & 128): [kernel][block][8] s_memrealtime
                                // (kernel 0 prep, 1 finish, 2 fix-up, 3 the rank GEMM's tiles)

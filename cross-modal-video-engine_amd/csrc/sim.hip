@@ -88,6 +88,15 @@ struct SimArgs {
   // from the undecided list -- a GT item's score never exceeds its row's best GT score, so it is never counted
   const int* row_gt1;
   const int* col_gt1;
+  // K14 at G64 (the ring kernel): the undecided pairs are re-scored in fp64 inside the epilogue (fixup_walk's
+  // arithmetic, wave_cos64 on the raw rows) instead of being listed for a fix-up launch
+  int fix_inline;
+  int q_f64, g_f64;
+  const void* q_raw;
+  const void* g_raw;
+  int64_t q_ld, g_ld, d;
+  const double* q_inv;
+  const double* g_inv;
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
@@ -255,16 +264,22 @@ __device__ __forceinline__ void plane_of(int tp, bool& a_lo, bool& b_lo, int& kt
 // the LDS-DMA loads write, and the compiler orders an LDS access after in-flight LDS-DMA (vmcnt(0))
 // only when it may alias that object -- with one shared dynamic object, the first epilogue LDS op
 // drained the next tile's prefetch.
-template <int BM, int BN, bool RANK>
+template <int BM, int BN, bool RANK, bool INL = false>
 struct EpiLds {
   int rc[BM];
   int cc[BN];
   float thr[2 * (BM + BN)];  // [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
+  double sgt[INL ? BM + BN : 1];  // inline fix-up (G64 K14): the rows' / columns' exact GT scores
+  uint32_t list[INL ? 1024 : 1];  // inline fix-up: the tile's undecided pairs (lr | lc << 8 | flags << 16)
+  int wtot[INL ? 16 : 1];         // inline fix-up: per-wave pair counts
 };
-template <int BM, int BN>
-struct EpiLds<BM, BN, false> {
+template <int BM, int BN, bool INL>
+struct EpiLds<BM, BN, false, INL> {
   int rc[1], cc[1];
   float thr[1];
+  double sgt[1];
+  uint32_t list[1];
+  int wtot[1];
 };
 
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
@@ -298,7 +313,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
                                          (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
 
-  __shared__ EpiLds<BM, BN, epi_thr(EPI)> epi;
+  // the G64 ring rank kernel re-scores its undecided pairs itself when the K14 host asks (SimArgs::fix_inline)
+  constexpr bool INL = EPI == EPI_RANK && NS > 2;
+  __shared__ EpiLds<BM, BN, epi_thr(EPI), INL> epi;
+  double sgt_pub = 0.0;  // INL: this thread's row / column GT score (tid < BM + BN), published with the thresholds
   int* lds_rc = epi.rc;
   int* lds_cc = epi.cc;
   float* lds_thr = epi.thr;
@@ -495,6 +513,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       if (tid < BM + BN) {
         lds_thr[tid] = thr_hi_v;
         lds_thr[BM + BN + tid] = thr_lo_v;
+        if constexpr (INL) epi.sgt[tid] = sgt_pub;
       }
       CMVE_BAR_LDS();
       CMVE_STAMP(4);
@@ -701,6 +720,112 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
                                          : (a.tile_buckets ? (m0 >> 6) * a.nbn64 + (n0 >> 6) : (n0 >> CAND_BUCKET_SHIFT));
       unsigned long long wbase = 0ull;
       if (total && lane == 0) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
+      if constexpr (INL) {
+        if (a.fix_inline) {
+          // fp64 re-score of the tile's undecided pairs (fixup_walk's arithmetic: the same scores), counted
+          // into the tile's LDS counts before the flush: the pairs go to an LDS list (wave prefix + this
+          // lane's exclusive prefix) and the block's waves take them two at a time, every load of both pairs
+          // in flight at once (a pair costs one trip to the raw rows; a 1k-A tile holds ~6)
+          if (lane == 0) epi.wtot[wave] = (int)total;
+          CMVE_BAR_LDS();
+          int woff = 0, ntot = 0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const int t = epi.wtot[w];
+            woff += w < wave ? t : 0;
+            ntot += t;
+          }
+          const bool listed = ntot <= 1024;
+          if (listed && nmine) {
+            uint32_t slot = (uint32_t)woff + excl;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              uint32_t m = (und[i] | (und[i] >> 16)) & 0xffffu;
+              while (m) {
+                const int bit = __builtin_ctz(m);
+                m &= m - 1u;
+                const uint32_t lr = (uint32_t)(rbase - m0 + i * 16 + (bit & 3));
+                const uint32_t lc = (uint32_t)(cbase - n0 + (bit >> 2) * 16);
+                const uint32_t fl = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
+                epi.list[slot++] = lr | (lc << 8) | (fl << 16);
+              }
+            }
+          }
+          if (listed) {
+            CMVE_BAR_LDS();
+            auto rescore2 = [&](uint32_t e1, uint32_t e2, bool two) {
+              const int64_t r1 = m0 + (e1 & 0xff), c1 = n0 + ((e1 >> 8) & 0xff);
+              const int64_t r2 = two ? m0 + (e2 & 0xff) : r1, c2 = two ? n0 + ((e2 >> 8) & 0xff) : c1;
+              // the norms travel with the rows (loaded after the dot they were a second round trip)
+              const double inv1 = a.q_inv[r1] * a.g_inv[c1], inv2 = a.q_inv[r2] * a.g_inv[c2];
+              double d1, d2;
+              if (a.q_f64) {
+                const double* q = (const double*)a.q_raw;
+                if (a.g_f64) {
+                  const double* g = (const double*)a.g_raw;
+                  wave_dot64_x2(q + r1 * a.q_ld, g + c1 * a.g_ld, q + r2 * a.q_ld, g + c2 * a.g_ld, a.d, lane, d1, d2);
+                } else {
+                  const float* g = (const float*)a.g_raw;
+                  wave_dot64_x2(q + r1 * a.q_ld, g + c1 * a.g_ld, q + r2 * a.q_ld, g + c2 * a.g_ld, a.d, lane, d1, d2);
+                }
+              } else {
+                const float* q = (const float*)a.q_raw;
+                if (a.g_f64) {
+                  const double* g = (const double*)a.g_raw;
+                  wave_dot64_x2(q + r1 * a.q_ld, g + c1 * a.g_ld, q + r2 * a.q_ld, g + c2 * a.g_ld, a.d, lane, d1, d2);
+                } else {
+                  const float* g = (const float*)a.g_raw;
+                  wave_dot64_x2(q + r1 * a.q_ld, g + c1 * a.g_ld, q + r2 * a.q_ld, g + c2 * a.g_ld, a.d, lane, d1, d2);
+                }
+              }
+              if (lane == 0) {
+                const double s1 = d1 * inv1;  // wave_cos64
+                if ((e1 >> 16) & 1u) { if (s1 > epi.sgt[r1 - m0]) lds_add_u32_async(&lds_rc[r1 - m0], 1); }
+                if ((e1 >> 17) & 1u) { if (s1 > epi.sgt[BM + c1 - n0]) lds_add_u32_async(&lds_cc[c1 - n0], 1); }
+                if (two) {
+                  const double s2 = d2 * inv2;
+                  if ((e2 >> 16) & 1u) { if (s2 > epi.sgt[r2 - m0]) lds_add_u32_async(&lds_rc[r2 - m0], 1); }
+                  if ((e2 >> 17) & 1u) { if (s2 > epi.sgt[BM + c2 - n0]) lds_add_u32_async(&lds_cc[c2 - n0], 1); }
+                }
+              }
+            };
+            for (int p = 2 * wave; p < ntot; p += 2 * NW)
+              rescore2(epi.list[p], p + 1 < ntot ? epi.list[p + 1] : 0u, p + 1 < ntot);
+          } else {
+            // more than the list holds (a pathological tile): each wave re-scores its own pairs in turn
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              uint32_t bits = (und[i] | (und[i] >> 16)) & 0xffffu;
+              unsigned long long m;
+              while ((m = __builtin_amdgcn_ballot_w64(bits != 0u))) {
+                const int src = (int)__builtin_ctzll(m);
+                const uint32_t sb = (uint32_t)__builtin_amdgcn_readlane((int)bits, src);
+                const uint32_t su = (uint32_t)__builtin_amdgcn_readlane((int)und[i], src);
+                const int bit = __builtin_ctz(sb);
+                if (lane == src) bits &= bits - 1u;
+                const int lr = wr * (TM * 16) + (src >> 4) * 4 + i * 16 + (bit & 3);
+                const int lc = wc * (TN * 16) + (src & 15) + (bit >> 2) * 16;
+                const int64_t row = m0 + lr, col = n0 + lc;
+                const double inva = a.q_inv[row], invb = a.g_inv[col];
+                double sc;
+                if (a.q_f64) {
+                  const double* x = (const double*)a.q_raw + row * a.q_ld;
+                  sc = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane);
+                } else {
+                  const float* x = (const float*)a.q_raw + row * a.q_ld;
+                  sc = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane);
+                }
+                if (lane == 0) {
+                  if (((su >> bit) & 1u) && sc > epi.sgt[lr]) lds_add_u32_async(&lds_rc[lr], 1);
+                  if (((su >> (16 + bit)) & 1u) && sc > epi.sgt[BM + lc]) lds_add_u32_async(&lds_cc[lc], 1);
+                }
+              }
+            }
+          }
+        }
+      }
       CMVE_STAMP(6);
 #ifdef CMVE_DBG_NOFLUSH  // diagnostic build only: no global flush of candidates / counts (results garbage)
       for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
@@ -717,7 +842,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
         }
       }
-      if (total) {
+      bool emit = total != 0u;
+      if constexpr (INL) emit = emit && !a.fix_inline;  // (fixed above; the bucket count stays: the pair total)
+      if (emit) {
         unsigned long long slot = __shfl(wbase, 0, 64) + excl;
         unsigned long long* dst = a.cand + (size_t)bucket * a.cap_b;
   #pragma unroll
@@ -931,6 +1058,17 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   constexpr int LPS = (BM / 8 / NW + BN / 8 / NW) * (MODE == CMVE_SIM_BF16X3 ? 2 : 1);  // loads / stage / wave
   static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
   const int nk0 = a.nk0;
+  // K14: the other set's err_max shards as VECTOR loads, one shard per lane, issued before the first
+  // K-tiles (the oldest loads: retired by the first ring wait) and folded after the main loop -- as scalar
+  // loads their round trip held the prologue (~2.5 us to the first K-tile in the stamps)
+  static_assert(EVAL_EMAX_SHARDS == 64, "one err_max shard per lane");
+  unsigned emq = 0u, emg = 0u;
+  if constexpr (epi_thr(EPI)) {
+    if (a.thr_gt) {
+      emq = a.q_emax[lane];
+      emg = a.g_emax[lane];
+    }
+  }
   for (int t = 0; t < NS - 1 && t < nk0; ++t) stage(t, t);
   // K14 thresholds: the GT score / bound loads are issued behind the first K-tiles' loads and the rule
   // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
@@ -939,7 +1077,6 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   const bool thr_dir = tid < BM ? a.row_hi != nullptr : (tid < BM + BN && a.col_hi != nullptr);
   if constexpr (epi_thr(EPI)) {
     if (a.thr_gt) {
-      reduce_err_max();  // scalar loads: retired by the first barrier's lgkmcnt(0)
       if (thr_dir) {
         sgt_raw = tid < BM ? a.row_sgt[m0 + tid] : a.col_sgt[n0 + tid - BM];
         e_raw = tid < BM ? a.q_err[m0 + tid] : a.g_err[n0 + tid - BM];
@@ -1013,7 +1150,17 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the threshold loads, if any are still out)
   if constexpr (epi_thr(EPI)) {
+    if (a.thr_gt) {  // fold the shards: a wave max (every lane the same bits)
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        emq = max(emq, (unsigned)__shfl_xor((int)emq, o, 64));
+        emg = max(emg, (unsigned)__shfl_xor((int)emg, o, 64));
+      }
+      qmax_v = __uint_as_float(emq);
+      gmax_v = __uint_as_float(emg);
+    }
     if (a.thr_gt && thr_dir) thr_of(sgt_raw, e_raw, tid < BM ? gmax_v : qmax_v, thr_hi_v, thr_lo_v);
+    if constexpr (INL) sgt_pub = sgt_raw;  // (after the main loop: the load has been waited for)
   }
   CMVE_STAMP(2);
   } else {
@@ -1141,6 +1288,12 @@ static bool sim_uses_phased(int mode, int64_t nq_pad, int64_t ng_pad) {
   const int force = sim_geo_force();
   if (force == 128 || nq_pad % 256 || ng_pad % 256 || (nq_pad / 256) * (ng_pad / 256) < 512) return false;
   return !(force == 2562 && mode != CMVE_SIM_BF16X3);
+}
+
+// true when launch_sim takes the G64 ring kernel (64 x 64 tiles: problems of fewer than 128 tiles of 128^2)
+static bool sim_uses_g64(int64_t nq_pad, int64_t ng_pad) {
+  return sim_geo_force() != 128 && !(nq_pad % 256 == 0 && ng_pad % 256 == 0 && (nq_pad / 256) * (ng_pad / 256) >= 512) &&
+         (nq_pad / 128) * (ng_pad / 128) < 128 && nq_pad % 64 == 0 && ng_pad % 64 == 0;
 }
 
 template <int MODE, int EPI>
@@ -1708,6 +1861,23 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     a.row_gt1 = sq.gt1;
     a.col_gt1 = sg.gt1;
   }
+  // G64 (1k-A scale): the rank GEMM re-scores its own undecided pairs (no list, no fix-up launch)
+  const char* fix_env = getenv("CMVE_EVAL_FIX_LAUNCH");  // kernel studies / tests: the separate fix-up launch
+  const bool no_inline = fix_env && atoi(fix_env) != 0;
+  const bool inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
+  if (inline_fix) {
+    a.fix_inline = 1;
+    a.q_f64 = qf;
+    a.g_f64 = gf;
+    a.q_raw = q->raw;
+    a.g_raw = g->raw;
+    a.q_ld = q->raw_ld;
+    a.g_ld = g->raw_ld;
+    a.d = q->d;
+    a.q_inv = q->inv_norm;
+    a.g_inv = g->inv_norm;
+    c.fix_inline = 1;
+  }
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
   if (!a.thr_gt) {
     EvalThrSide t0{a.row_sgt, a.q_err, a.g_emax, row_off ? sq.thr_hi : nullptr, sq.thr_lo, q->n_pad};
@@ -1722,9 +1892,16 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  arm(2);
-  st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
-  if (st) return st;
+  if (inline_fix) {  // (an empty span in the fix-up's timing slot)
+    if (kev) {
+      CMVE_HIP(hipEventRecord(kev[4], s));
+      CMVE_HIP(hipEventRecord(kev[5], s));
+    }
+  } else {
+    arm(2);
+    st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
+    if (st) return st;
+  }
   arm(3);
   st = cmve::launch_eval(sq, sg, c, qf, gf, 2, s);
   if (st) return st;
