@@ -58,15 +58,54 @@ __device__ __forceinline__ double lane_dot(const double (&v)[4][4], const double
   return dot;
 }
 
+// the wave sums of K independent values in ONE butterfly (wave_sum's pairings and order for each: the same
+// bits as K wave_sum calls, one reduction latency instead of K)
+template <int K>
+__device__ __forceinline__ void wave_sum_k(double (&v)[K]) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], o, 64);
+}
+
+// pack row `row` of side A (held in v) into its planes with 1/||x|| = inv, accumulating this lane's squared
+// residuals in acc (not yet reduced); pack_bounds stores inv and the bounds from the reduced sums
+__device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalCommon& c, int64_t row,
+                                               const double (&v)[4][4], double inv, int lane, PackAcc& acc);
+__device__ __forceinline__ bool pack_bf(const EvalSide& A, const EvalCommon& c) {
+  return !(c.mode == CMVE_SIM_F16 && A.h16 != nullptr);
+}
+__device__ __forceinline__ void pack_bounds(const EvalSide& A, int64_t row, double inv, bool bf, double e1, double e2,
+                                            double e3, int lane, float (&eb)[3]) {
+  if (lane == 0) {
+    A.inv[row] = inv;
+    // pack_row_planes' bounds
+    eb[0] = bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY;
+    eb[1] = bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY;
+    eb[2] = A.err_h16 ? f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12) : 0.f;
+    A.err_hi[row] = eb[0];
+    A.err_hilo[row] = eb[1];
+    if (A.err_h16) A.err_h16[row] = eb[2];
+  }
+}
+
 // pack row `row` of side A (held in v) into its planes with 1/||x|| = inv; lane 0 stores inv and the
 // bounds; eb = the row's bounds (lane 0)
 __device__ __forceinline__ void pack_regs(const EvalSide& A, const EvalCommon& c, int64_t row,
                                           const double (&v)[4][4], double inv, int lane, float (&eb)[3]) {
+  PackAcc acc;
+  pack_regs_lane(A, c, row, v, inv, lane, acc);
+  const bool bf = pack_bf(A, c);
+  const double e1 = bf ? wave_sum(acc.e1) : 0.0, e2 = bf ? wave_sum(acc.e2) : 0.0, e3 = wave_sum(acc.e3);
+  pack_bounds(A, row, inv, bf, e1, e2, e3, lane, eb);
+}
+
+__device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalCommon& c, int64_t row,
+                                               const double (&v)[4][4], double inv, int lane, PackAcc& acc) {
   uint16_t* hrow = A.hi + row * c.d_pad;
   uint16_t* lrow = A.lo ? A.lo + row * c.d_pad : nullptr;
   uint16_t* frow = A.h16 ? A.h16 + row * c.d_pad : nullptr;
   const bool want_f16 = frow != nullptr;
-  PackAcc acc;
   if (c.mode == CMVE_SIM_F16 && want_f16) {
     // the F16 rank GEMM reads only the fp16 plane: the bf16 planes are not written and their bounds
     // are +inf (a stale plane can never pass for a bounded one)
@@ -107,18 +146,6 @@ __device__ __forceinline__ void pack_regs(const EvalSide& A, const EvalCommon& c
       if (lrow) *(cmve_u16x4*)(lrow + k) = lv;
       if (frow) *(cmve_u16x4*)(frow + k) = fv;
     }
-  }
-  const bool bf = !(c.mode == CMVE_SIM_F16 && want_f16);
-  const double e1 = bf ? wave_sum(acc.e1) : 0.0, e2 = bf ? wave_sum(acc.e2) : 0.0, e3 = wave_sum(acc.e3);
-  if (lane == 0) {
-    A.inv[row] = inv;
-    // pack_row_planes' bounds
-    eb[0] = bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY;
-    eb[1] = bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY;
-    eb[2] = A.err_h16 ? f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12) : 0.f;
-    A.err_hi[row] = eb[0];
-    A.err_hilo[row] = eb[1];
-    if (A.err_h16) A.err_h16[row] = eb[2];
   }
 }
 
@@ -335,11 +362,27 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, Eva
       double v[4][4], w[4][4];
       load_row_regs((const TQ*)q.raw + i * q.ld, c.d, lane, v);
       load_row_regs((const TG*)g.raw + p * g.ld, c.d, lane, w);
-      const double ssq = wave_sum(lane_sumsq(v, c.d, lane)), ssg = wave_sum(lane_sumsq(w, c.d, lane));
-      const double invq = row_inv_norm(ssq, q.eps, q.flags), invg = row_inv_norm(ssg, g.eps, g.flags);
-      pack_regs(q, c, i, v, invq, lane, ebq);
-      pack_regs(g, c, p, w, invg, lane, ebg);
-      const double s = wave_sum(lane_dot(v, w, c.d, lane)) * (invq * invg);
+      // both norms and the pair's dot in one butterfly, then both planes' residual sums in another (each sum
+      // in wave_sum's order: the bits of the separate reductions)
+      double r3[3] = {lane_sumsq(v, c.d, lane), lane_sumsq(w, c.d, lane), lane_dot(v, w, c.d, lane)};
+      wave_sum_k<3>(r3);
+      const double invq = row_inv_norm(r3[0], q.eps, q.flags), invg = row_inv_norm(r3[1], g.eps, g.flags);
+      PackAcc aq, ag;
+      pack_regs_lane(q, c, i, v, invq, lane, aq);
+      pack_regs_lane(g, c, p, w, invg, lane, ag);
+      const bool bfq = pack_bf(q, c), bfg = pack_bf(g, c);
+      if (!bfq && !bfg) {  // the F16 rank GEMM's planes: only the fp16 residuals
+        double e[2] = {aq.e3, ag.e3};
+        wave_sum_k<2>(e);
+        pack_bounds(q, i, invq, false, 0.0, 0.0, e[0], lane, ebq);
+        pack_bounds(g, p, invg, false, 0.0, 0.0, e[1], lane, ebg);
+      } else {
+        double e[6] = {aq.e1, aq.e2, aq.e3, ag.e1, ag.e2, ag.e3};
+        wave_sum_k<6>(e);
+        pack_bounds(q, i, invq, bfq, bfq ? e[0] : 0.0, bfq ? e[1] : 0.0, e[2], lane, ebq);
+        pack_bounds(g, p, invg, bfg, bfg ? e[3] : 0.0, bfg ? e[4] : 0.0, e[5], lane, ebg);
+      }
+      const double s = r3[2] * (invq * invg);
       if (lane == 0) {  // a one-entry list: its score, or +inf when it is NaN (prep_row_regs' encoding)
         q.sgt[i] = s == s ? s : (double)INFINITY;
         g.sgt[p] = s == s ? s : (double)INFINITY;

@@ -719,7 +719,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
       const int bucket = EPI == EPI_TOPK ? (m0 >> 8)
                                          : (a.tile_buckets ? (m0 >> 6) * a.nbn64 + (n0 >> 6) : (n0 >> CAND_BUCKET_SHIFT));
       unsigned long long wbase = 0ull;
-      if (total && lane == 0) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
+      bool inl = false;  // inline fix-up: the pair total is added after the flush (a returning atomic here stayed
+                         // in vmcnt, so the re-score's first load wait also waited for its round trip)
+      if constexpr (INL) inl = a.fix_inline != 0;
+      if (total && lane == 0 && !inl) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
       if constexpr (INL) {
         if (a.fix_inline) {
           // fp64 re-score of the tile's undecided pairs (fixup_walk's arithmetic: the same scores), counted
@@ -842,8 +845,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
           if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
         }
       }
-      bool emit = total != 0u;
-      if constexpr (INL) emit = emit && !a.fix_inline;  // (fixed above; the bucket count stays: the pair total)
+      if (inl && total && lane == 0) atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);  // (no return)
+      const bool emit = total != 0u && !inl;  // (inline: re-scored above; the bucket count is the pair total)
       if (emit) {
         unsigned long long slot = __shfl(wbase, 0, 64) + excl;
         unsigned long long* dst = a.cand + (size_t)bucket * a.cap_b;
