@@ -21,6 +21,7 @@ struct cmve_handle {
   hipEvent_t eval_ev[CMVE_EVAL_TIMING_SLOTS][4] = {};
   // kernel-exact timing of the same evaluations: start / stop of each of the four launches
   hipEvent_t eval_kev[CMVE_EVAL_TIMING_SLOTS][8] = {};
+  bool eval_no_fix[CMVE_EVAL_TIMING_SLOTS] = {};  // the slot's evaluation had no fix-up launch (re-scored in the GEMM)
   // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
   void* scratch = nullptr;
   size_t scratch_bytes = 0;

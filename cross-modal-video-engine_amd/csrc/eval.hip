@@ -477,29 +477,45 @@ __global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSid
     EVAL_STAMP(c, 1, 1);
     return;
   }
-  unsigned long long acc[8] = {};
+  // per wave: #rank <= 1 / 5 / 10 from ballots (no reduction), the rank sums in one butterfly of both
+  // directions; then one LDS round over the block's waves and 8 lanes adding into the stats head
   const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t rq = 0, rg = 0;
   if (q.off && i < q.n) {
-    const int64_t r = gt_rank_of(q.cnt[i], q.sgt[i], g.n);
-    q.ranks[i] = r;
-    acc[0] = (r <= 1);
-    acc[1] = (r <= 5);
-    acc[2] = (r <= 10);
-    acc[3] = (unsigned long long)r;
+    rq = gt_rank_of(q.cnt[i], q.sgt[i], g.n);
+    q.ranks[i] = rq;
   }
   if (g.off && i < g.n) {
-    const int64_t r = gt_rank_of(g.cnt[i], g.sgt[i], q.n);
-    g.ranks[i] = r;
-    acc[4] = (r <= 1);
-    acc[5] = (r <= 5);
-    acc[6] = (r <= 10);
-    acc[7] = (unsigned long long)r;
+    rg = gt_rank_of(g.cnt[i], g.sgt[i], q.n);
+    g.ranks[i] = rg;
   }
-  block_reduce_k<false>(acc, red);
-  if (threadIdx.x == 0) {
+  unsigned long long sq = (unsigned long long)rq, sg = (unsigned long long)rg;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((k < 4 ? q.off : g.off) && acc[k]) atomicAdd((unsigned long long*)&c.stats[k], acc[k]);
+  for (int o = 32; o >= 1; o >>= 1) {
+    sq += __shfl_xor(sq, o, 64);
+    sg += __shfl_xor(sg, o, 64);
+  }
+  const unsigned long long w[8] = {
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rq != 0 && rq <= 1)),
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rq != 0 && rq <= 5)),
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rq != 0 && rq <= 10)), sq,
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rg != 0 && rg <= 1)),
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rg != 0 && rg <= 5)),
+      (unsigned long long)__builtin_popcountll(__builtin_amdgcn_ballot_w64(rg != 0 && rg <= 10)), sg};
+  if (lane < 8) {
+    unsigned long long v = w[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = lane == k ? w[k] : v;
+    red[lane * FIN_NW + wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    const int k = threadIdx.x;
+    unsigned long long a = red[k * FIN_NW];
+#pragma unroll
+    for (int ww = 1; ww < FIN_NW; ++ww) a += red[k * FIN_NW + ww];
+    if ((k < 4 ? q.off : g.off) && a) atomicAdd((unsigned long long*)&c.stats[k], a);
   }
   EVAL_STAMP(c, 1, 1);
 }

@@ -1895,12 +1895,8 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  if (inline_fix) {  // (an empty span in the fix-up's timing slot)
-    if (kev) {
-      CMVE_HIP(hipEventRecord(kev[4], s));
-      CMVE_HIP(hipEventRecord(kev[5], s));
-    }
-  } else {
+  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = inline_fix;
+  if (!inline_fix) {
     arm(2);
     st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
     if (st) return st;
@@ -1976,6 +1972,12 @@ extern "C" int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4
   hipEvent_t* kev = h->eval_kev[slot];
   CMVE_REQUIRE(kev[0] && kev[7], "cmve_eval_kernel_timing: slot %d never recorded", slot);
   CMVE_HIP(hipEventSynchronize(kev[7]));
-  for (int k = 0; k < 4; ++k) CMVE_HIP(hipEventElapsedTime(&ms4[k], kev[2 * k], kev[2 * k + 1]));
+  for (int k = 0; k < 4; ++k) {
+    if (k == 2 && h->eval_no_fix[slot]) {  // no fix-up launch: its pairs were re-scored inside the rank GEMM
+      ms4[k] = 0.f;
+      continue;
+    }
+    CMVE_HIP(hipEventElapsedTime(&ms4[k], kev[2 * k], kev[2 * k + 1]));
+  }
   return CMVE_OK;
 }

@@ -372,13 +372,16 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
                   int64_t* ranks, int64_t* recall);
 
 /*
- * K14 -- one exact two-direction GT-rank evaluation of a resident problem in FOUR launches
+ * K14 -- one exact two-direction GT-rank evaluation of a resident problem in three or four launches
  * (the reference's per-validation chain LINAS-engine/validate.py:61-74 / tester.py:133-139:
  * evaluation.cal_error (evaluation.py:17-21) then util/metrics.eval_q2m t2v and v2t (metrics.py:124-157)).
  *   launch 1: pack q and g from their raw rows (as cmve_pack_rows), exact fp64 GT scores of both
  *             directions (as cmve_gt_thresholds), zeroed counters, err_max shards;
  *   launch 2: the fused rank GEMM (as cmve_rank_mfma), deriving the rank thresholds from the GT scores
  *             and the err_max shards in-kernel (a G256-sized problem gets them from one more small launch);
+ *             each row's first GT pair is dropped from the undecided pairs (it is never counted); at G64
+ *             size (fewer than 128 tiles of 128^2, e.g. MSR-VTT-1kA) the kernel re-scores its undecided pairs
+ *             in fp64 itself (cmve_rank_fixup's arithmetic) and launch 3 is skipped;
  *   launch 3: the fp64 fix-up (as cmve_rank_fixup);
  *   launch 4: the ranks (as cmve_gt_ranks), R@K sums, the pair total and the sets' err_max.
  * The numbers equal the separate-launch path bit for bit.  q/g: packed sets (their planes, norms and
@@ -407,7 +410,8 @@ int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mod
 int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3);
 /* the same evaluation's four kernel durations (ms4: prep, rank GEMM, fix-up, finish), each from its own
  * launch's start / stop (hipExtLaunchKernelGGL: the dispatch timestamps rocprofv3 reports, without the
- * dispatch gaps that events recorded between launches include); synchronises on the slot */
+ * dispatch gaps that events recorded between launches include; fix-up 0 when it ran inside the rank GEMM);
+ * synchronises on the slot */
 int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
 /* Graph form of cmve_eval_ranks for an evaluation repeated on fixed buffers (the reference re-runs
  * validate.py:61-74 on new embeddings written into the same encode_* buffers; the bench's pipelined
