@@ -521,6 +521,36 @@ def test_bench_shape_ranks_against_independent_fp64(torch_cuda):
     assert np.array_equal(got, exp), np.nonzero(got != exp)
 
 
+@pytest.mark.parametrize("paired", [True, False])
+def test_inline_fixup_dense_tiles(torch_cuda, paired):
+    """The G64 rank GEMM's inline fp64 re-score when tiles are dense with undecided pairs: 160 near-duplicate
+    captions / videos (one vector + 1e-4 noise: every pair among them lies inside the fp16 band, their scores
+    ~1e-8 apart -- far above fp64 rounding, so the oracle's order is the exact one) make the
+    4 x 4 tiles over them carry ~4,096 pairs each -- past the 1,024-entry LDS list, so those tiles take the
+    per-wave path -- and the ragged tiles next to them fewer.  Ranks == the oracle's exact counts, with the
+    one-to-one pairing (paired prep) and with a multi-GT v2t side (general prep)."""
+    import torch
+    from cmve import engine
+    rng = np.random.default_rng(91)
+    n, d, k = 1000, 256, 160
+    v = rng.standard_normal((n, d))
+    v[:k] = v[0] + 1e-4 * rng.standard_normal((k, d))
+    c = v + 0.8 * rng.standard_normal((n, d))
+    c[:k] = v[0] + 1e-4 * rng.standard_normal((k, d))
+    t2v = [[i] for i in range(n)]
+    if paired:
+        v2t = [[j] for j in range(n)]
+    else:
+        v2t = [[j, (j + 1) % n] if j % 3 == 0 else [j] for j in range(n)]
+    s = R.exact_scores64(c, v)
+    exp_r, exp_c = R.rank_counts(s, t2v), R.rank_counts(s.T, v2t)
+    sess = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64)
+    assert sess.paired == paired
+    r, cc = sess.run(torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    assert sess.ncand > 4 * 1024  # the dense tiles went past the LDS list
+    assert np.array_equal(r, exp_r) and np.array_equal(cc, exp_c)
+
+
 @pytest.mark.parametrize("nq,ng,d", [(3, 129, 100), (130, 257, 64), (1000, 1000, 1024), (257, 300, 1536),
                                      (2000, 600, 512), (64, 5000, 128), (4096, 8192, 64)])
 def test_rank_session_shapes_against_oracle(torch_cuda, nq, ng, d):
