@@ -317,7 +317,8 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide
     const int side = (int64_t)blockIdx.x * PREP_NW < q.n_pad ? 0 : 1;
     unsigned* sh = &c.emax[(side * 3 + threadIdx.x) * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];
     // +inf (a plane the mode does not write) is the largest value: a plain store equals the atomic max
-    if (m == INFINITY) *sh = __float_as_uint(m);
+    if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
+    } else if (m == INFINITY) *sh = __float_as_uint(m);
     else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
   }
   EVAL_STAMP(c, 0, 1);
@@ -407,7 +408,8 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, Eva
 #pragma unroll
     for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
     unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];  // [side][plane] = tid
-    if (m == INFINITY) *sh = __float_as_uint(m);
+    if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
+    } else if (m == INFINITY) *sh = __float_as_uint(m);
     else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
   }
   EVAL_STAMP(c, 0, 1);

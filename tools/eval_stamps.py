@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-os.environ["CMVE_EVAL_DBG"] = "128"
+os.environ["CMVE_EVAL_DBG"] = str(128 | int(os.environ.get("STAMPS_DBG", "0")))  # + study bits (results garbage)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "cross-modal-video-engine_amd"), ROOT, os.path.join(ROOT, "tests", "golden")):
     sys.path.insert(0, p)
@@ -24,9 +24,12 @@ def main():
     f.restype, f.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]
     buf = np.zeros(4 * 1024 * 8, np.uint64)
     res = []
+    warm = int(os.environ.get("STAMPS_WARM", "0"))  # evaluations enqueued just before the stamped one (GPU busy)
     for it in range(30):
         buf[:] = 0
         torch.cuda.synchronize()
+        for _ in range(warm):
+            sess.enqueue(ct, vt)
         sess.enqueue(ct, vt)
         torch.cuda.synchronize()
         _lib.check(f(buf.ctypes.data, buf.nbytes))
@@ -49,6 +52,7 @@ def main():
             if not live.any():
                 continue
             rel = (s[live] - t_ref) * 0.01  # us
+            out[name + "_start_pct"] = {f"p{q}": float(np.percentile(rel[:, 0], q)) for q in (10, 50, 90, 99)}
             out[name] = {"blocks": int(live.sum()), "start_first": float(rel[:, 0].min()),
                          "start_last": float(rel[:, 0].max()), "end_first": float(rel[:, 1].min()),
                          "end_last": float(rel[:, 1].max()), "work_med": float(np.median(rel[:, 1] - rel[:, 0]))}
