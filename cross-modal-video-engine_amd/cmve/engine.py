@@ -734,21 +734,20 @@ def _topk_dense_exact(q: RowSet, g: RowSet, k: int, gallery_chunk: int = 1 << 16
     """Exact top-k by dense fp64 scoring (the fallback of topk when an error band overflows): the
     normalised rows in fp64, gallery chunks scored by the K10 DOT kernel (a k-ordered fp64 fma chain
     per pair, so exact duplicates score identically -- a library dgemm rounds by tile position), each
-    chunk stable-sorted (score desc, index asc; NaN last as np.argsort of the errors) and merged with
-    the running top-k."""
+    chunk merged with the running top-k by K12f (cmve_topk_dense_merge: radix select + bitonic sort on the
+    device, score desc, index asc, NaN last as np.argsort of the errors)."""
     qn = q.normalized(torch.float64)
-    best_s = torch.full((q.n, 0), float("-inf"), dtype=torch.float64, device=q.device)
-    best_i = torch.zeros((q.n, 0), dtype=torch.int64, device=q.device)
     gn_all = g.normalized(torch.float64)
+    bufs = [(torch.empty((q.n, k), dtype=torch.float64, device=q.device),
+             torch.empty((q.n, k), dtype=torch.int64, device=q.device)) for _ in range(2)]
+    kb, cur = 0, 0
     for j0 in range(0, g.n, gallery_chunk):
         s = pairwise(qn, gn_all[j0:j0 + gallery_chunk].contiguous(), _lib.PW_DOT, 1.0, 0.0, torch.float64)
-        s = torch.nan_to_num(s, nan=float("-inf"))
-        cs, ci = torch.sort(s, dim=1, descending=True, stable=True)
-        cs, ci = cs[:, :k], ci[:, :k] + j0
-        # earlier chunks hold lower indices: [best | chunk] is index-ascending among equal scores
-        ms, mi = torch.cat([best_s, cs], 1), torch.cat([best_i, ci], 1)
-        o = torch.sort(ms, dim=1, descending=True, stable=True).indices[:, :k]
-        best_s, best_i = ms.gather(1, o), mi.gather(1, o)
+        (bs, bi), (os_, oi) = bufs[cur], bufs[1 - cur]
+        check(lib.cmve_topk_dense_merge(handle(q.device), _ptr(bs), _ptr(bi), kb, _ptr(s), s.stride(0), q.n,
+                                        s.shape[1], j0, k, _ptr(os_), _ptr(oi)), "cmve_topk_dense_merge")
+        kb, cur = k, 1 - cur
+    best_s, best_i = bufs[cur]
     return best_i.to(torch.int32), best_s
 
 

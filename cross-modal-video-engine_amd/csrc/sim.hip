@@ -229,7 +229,10 @@ constexpr size_t stage_bytes() {
 // 31.0 -> 26.6 us per evaluation, tools/eval_pipe.py)
 template <int MODE, int BM, int BN, bool PHASED>
 constexpr int ring_stages() {
-  return (PHASED || BM != 64 || BN != 64) ? 2 : 4;
+#ifndef CMVE_G64_STAGES
+#define CMVE_G64_STAGES 4
+#endif
+  return (PHASED || BM != 64 || BN != 64) ? 2 : CMVE_G64_STAGES;
 }
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
@@ -264,13 +267,16 @@ __device__ __forceinline__ void plane_of(int tp, bool& a_lo, bool& b_lo, int& kt
 // the LDS-DMA loads write, and the compiler orders an LDS access after in-flight LDS-DMA (vmcnt(0))
 // only when it may alias that object -- with one shared dynamic object, the first epilogue LDS op
 // drained the next tile's prefetch.
+#ifndef CMVE_INL_LIST
+#define CMVE_INL_LIST 1024
+#endif
 template <int BM, int BN, bool RANK, bool INL = false>
 struct EpiLds {
   int rc[BM];
   int cc[BN];
   float thr[2 * (BM + BN)];  // [0,BM) row_hi, [BM,BM+BN) col_hi, then the lo halves
   double sgt[INL ? BM + BN : 1];  // inline fix-up (G64 K14): the rows' / columns' exact GT scores
-  uint32_t list[INL ? 1024 : 1];  // inline fix-up: the tile's undecided pairs (lr | lc << 8 | flags << 16)
+  uint32_t list[INL ? CMVE_INL_LIST : 1];  // inline fix-up: the tile's undecided pairs (lr | lc << 8 | flags << 16)
   int wtot[INL ? 16 : 1];         // inline fix-up: per-wave pair counts
 };
 template <int BM, int BN, bool INL>
@@ -282,8 +288,11 @@ struct EpiLds<BM, BN, false, INL> {
   int wtot[1];
 };
 
+#ifndef CMVE_G64_BLOCKS
+#define CMVE_G64_BLOCKS 2
+#endif
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
-__global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
+__global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2) void sim_kernel(SimArgs a) {
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -738,7 +747,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void sim_kernel(SimArgs a) {
             woff += w < wave ? t : 0;
             ntot += t;
           }
-          const bool listed = ntot <= 1024;
+          const bool listed = ntot <= CMVE_INL_LIST;
           if (listed && nmine) {
             uint32_t slot = (uint32_t)woff + excl;
 #pragma unroll

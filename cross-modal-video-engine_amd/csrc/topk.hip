@@ -814,3 +814,179 @@ extern "C" int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve
 #undef TB
   return check_launch("topk_batch_finish_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// K12f: the exact dense top-k of topk's band-overflow fallback (engine._topk_dense_exact): per query row,
+// the k best of [its running best (kb entries, global ids) | a chunk of fp64 scores (ids j0 + c)] by (score
+// desc, id asc) -- the order of np.argsort on the errors with NaN last (NaN scores count as -inf, as the
+// caller's nan_to_num, and -0.0 as +0.0).  One block per row: an MSD radix select on the 64-bit
+// order-preserving score key finds the k-th largest key T and how many entries equal to T enter, a second
+// radix select on the ids among the keys == T picks the smallest of those ids, and the k winners are
+// bitonic-sorted in LDS.  A rare path (near-duplicate gallery rows): ~13 passes over the row from L2.
+// ---------------------------------------------------------------------------
+constexpr int TD_THREADS = 256;
+constexpr int TD_KMAX = 2048;
+
+__device__ __forceinline__ uint64_t td_key(double s) {  // larger score -> larger key
+  if (s != s) s = -INFINITY;
+  if (s == 0.0) s = 0.0;  // -0.0 ties +0.0, as the comparison sort
+  const uint64_t u = (uint64_t)__double_as_longlong(s);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ __launch_bounds__(TD_THREADS) void topk_dense_kernel(const double* __restrict__ best_s,
+                                                                const int64_t* __restrict__ best_i, int64_t kb,
+                                                                const double* __restrict__ s, int64_t lds,
+                                                                int64_t nc, int64_t j0, int k,
+                                                                double* __restrict__ out_s,
+                                                                int64_t* __restrict__ out_i) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_want;
+  __shared__ uint32_t n_sel;
+  __shared__ uint64_t wk[TD_KMAX];
+  __shared__ int64_t wi[TD_KMAX];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t N = kb + nc;
+  const int keff = (int)(N < k ? N : k);
+  auto cand = [&](int64_t c, uint64_t& key, int64_t& id) {
+    if (c < kb) {
+      key = td_key(best_s[row * kb + c]);
+      id = best_i[row * kb + c];
+    } else {
+      key = td_key(s[row * lds + (c - kb)]);
+      id = j0 + (c - kb);
+    }
+  };
+  // radix-select the keff-th largest key: `want` = its rank among the keys matching the prefix so far
+  if (tid == 0) {
+    s_prefix = 0ull;
+    s_want = (uint32_t)keff;
+  }
+  uint64_t mask = 0ull;
+  for (int shift = 56; shift >= 0 && keff < N && keff > 0; shift -= 8) {
+    for (int b = tid; b < 256; b += TD_THREADS) hist[b] = 0u;
+    __syncthreads();
+    const uint64_t prefix = s_prefix;
+    for (int64_t c = tid; c < N; c += TD_THREADS) {
+      uint64_t key;
+      int64_t id;
+      cand(c, key, id);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t want = s_want, acc = 0u;
+      int dgt = 255;
+      while (acc + hist[dgt] < want) acc += hist[dgt--];
+      s_want = want - acc;
+      s_prefix = prefix | ((uint64_t)dgt << shift);
+    }
+    mask |= 0xffull << shift;
+    __syncthreads();
+  }
+  // T = s_prefix (all 64 bits fixed); take every key > T and the s_want smallest ids among the keys == T.
+  // The tied ids are radix-selected (ascending) the same way: their s_want-th smallest id is idT.
+  const bool all = keff >= N;
+  const uint64_t T = s_prefix;
+  __shared__ uint64_t s_idpre;
+  __shared__ uint32_t s_idwant;
+  if (tid == 0) {
+    s_idpre = 0ull;
+    s_idwant = s_want;
+  }
+  __syncthreads();
+  uint64_t imask = 0ull;
+  for (int shift = 56; shift >= 0 && !all && keff > 0; shift -= 8) {
+    for (int b = tid; b < 256; b += TD_THREADS) hist[b] = 0u;
+    __syncthreads();
+    const uint64_t pre = s_idpre;
+    for (int64_t c = tid; c < N; c += TD_THREADS) {
+      uint64_t key;
+      int64_t id;
+      cand(c, key, id);
+      if (key == T && (((uint64_t)id) & imask) == pre) atomicAdd(&hist[(((uint64_t)id) >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t want = s_idwant, acc = 0u;
+      int dgt = 0;
+      while (acc + hist[dgt] < want) acc += hist[dgt++];
+      s_idwant = want - acc;
+      s_idpre = pre | ((uint64_t)dgt << shift);
+    }
+    imask |= 0xffull << shift;
+    __syncthreads();
+  }
+  const uint64_t idT = s_idpre;
+  if (tid == 0) n_sel = 0u;
+  __syncthreads();
+  for (int64_t c = tid; c < N; c += TD_THREADS) {
+    uint64_t key;
+    int64_t id;
+    cand(c, key, id);
+    if (all || key > T || (key == T && (uint64_t)id <= idT)) {
+      const uint32_t p = atomicAdd(&n_sel, 1u);
+      if (p < (uint32_t)TD_KMAX) {
+        wk[p] = key;
+        wi[p] = id;
+      }
+    }
+  }
+  __syncthreads();
+  int P = 1;
+  while (P < keff) P <<= 1;
+  for (int t = (int)n_sel + tid; t < P; t += TD_THREADS) {  // padding sorts last
+    wk[t] = 0ull;
+    wi[t] = INT64_MAX;
+  }
+  __syncthreads();
+  // bitonic sort, "before" = (key desc, id asc)
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < P; t += TD_THREADS) {
+        const int o = t ^ stride;
+        if (o > t) {
+          const bool up = (t & size) == 0;
+          const bool before_o = wk[o] > wk[t] || (wk[o] == wk[t] && wi[o] < wi[t]);
+          if (before_o == up) {
+            const uint64_t k2 = wk[t];
+            wk[t] = wk[o];
+            wk[o] = k2;
+            const int64_t i2 = wi[t];
+            wi[t] = wi[o];
+            wi[o] = i2;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int t = tid; t < k; t += TD_THREADS) {
+    if (t < keff) {
+      const uint64_t kk = wk[t];
+      const uint64_t u = (kk & 0x8000000000000000ull) ? (kk & 0x7fffffffffffffffull) : ~kk;
+      out_s[row * k + t] = __longlong_as_double((long long)u);
+      out_i[row * k + t] = wi[t];
+    } else {
+      out_s[row * k + t] = -INFINITY;
+      out_i[row * k + t] = -1;
+    }
+  }
+}
+
+extern "C" int cmve_topk_dense_merge(cmve_handle_t h, const double* best_s, const int64_t* best_i, int64_t kb,
+                                     const double* scores, int64_t lds, int64_t n_rows, int64_t nc, int64_t j0,
+                                     int32_t k, double* out_s, int64_t* out_i) {
+  CMVE_REQUIRE(h && (kb == 0 || (best_s && best_i)) && (nc == 0 || scores) && out_s && out_i,
+               "cmve_topk_dense_merge: NULL argument");
+  CMVE_REQUIRE(k >= 1 && k <= TD_KMAX && kb >= 0 && kb <= k && nc >= 0 && n_rows >= 0 && lds >= nc && j0 >= 0,
+               "cmve_topk_dense_merge: bad shape (1 <= k <= %d, 0 <= kb <= k)", TD_KMAX);
+  CMVE_REQUIRE(kb + nc < (1ll << 32), "cmve_topk_dense_merge: more than 2^32 candidates per row");
+  if (n_rows == 0) return CMVE_OK;
+  CMVE_REQUIRE((const void*)out_s != (const void*)best_s && (const void*)out_i != (const void*)best_i,
+               "cmve_topk_dense_merge: out must not alias the running best");
+  hipLaunchKernelGGL(topk_dense_kernel, dim3((unsigned)n_rows), dim3(TD_THREADS), 0, h->stream, best_s, best_i, kb,
+                     scores, lds, nc, j0, (int)k, out_s, out_i);
+  return check_launch("topk_dense_kernel");
+}

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 14
+#define CMVE_ABI_VERSION 15
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -535,6 +535,15 @@ int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32
  */
 int cmve_topk_batch_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int32_t k, int64_t* sample_rows,
                               int64_t* n_floats);
+/* K12f: the exact dense top-k step of topk's band-overflow fallback (a query whose error band holds more
+ * than the candidate cap: near-duplicate gallery rows; engine._topk_dense_exact scores gallery chunks in
+ * fp64 with cmve_pairwise DOT).  Per row: the k best of [best_s / best_i (kb <= k entries, global ids) |
+ * scores[row, 0..nc) with ids j0 + c] by (score desc, id asc) -- np.argsort's order of the errors, NaN
+ * last (as -inf), -0.0 == +0.0 -- into out_s / out_i [n_rows, k] (ids -1 / -inf past the candidates).
+ * The reference's inference.py:79-80 full argsort, for the rows the fast path cannot decide. */
+int cmve_topk_dense_merge(cmve_handle_t h, const double* best_s, const int64_t* best_i, int64_t kb,
+                          const double* scores, int64_t lds, int64_t n_rows, int64_t nc, int64_t j0, int32_t k,
+                          double* out_s, int64_t* out_i);
 int cmve_topk_batch(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t k,
                     float* ws, int64_t ws_floats, int32_t* out_idx, double* out_score, int32_t* unresolved);
 

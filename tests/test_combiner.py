@@ -181,3 +181,50 @@ def test_gpu_transpose_blocks_shapes(R, C):
     op = engine.PackedOperand.from_blocks_transposed(y.view(9, R, C), R, C)
     rs = engine.RowSet(ref.contiguous(), with_lo=True, with_f16=False, raw_rows=True)
     assert torch.equal(op.hi[:rs.n_pad], rs.hi) and torch.equal(op.lo[:rs.n_pad], rs.lo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,f,gs,B", [(640, 8, 32, 64), (512, 4, 5, 15), (640, 2, 7, 7)])
+def test_gpu_mha_absorbed_against_fp64(d, f, gs, B):
+    """cmve_mha_absorbed (K9b) through the C ABI against an fp64 torch restatement of its contract: key t of
+    query qb = g*gs + bb is run R % L of conv block g*gs*f + R / L (R = t*gs + bb) of y [B*f*16, C = d];
+    z_h = sum_t softmax_t(u_h . n_t) n_t with n_t the un-affined LayerNorm of the key (eps 1e-5), in the kernel's
+    element order (e = p*cpr + c' <-> original c'*16 + p), and v.mean(0) in the original order."""
+    import torch
+    from cmve import engine
+    from cmve._lib import lib, check
+    H, npix = 8, 16
+    cpr, L = d // npix, d // (d // npix)
+    T = f * L
+    gen = torch.Generator().manual_seed(d + f + gs)
+    y = torch.relu(torch.randn(B * f * npix, d, generator=gen, dtype=torch.float64))
+    u = torch.randn(B, H * d, generator=gen, dtype=torch.float64) * 0.05
+    yc, uc = y.float().cuda(), u.float().cuda()
+    z = torch.empty(B, H * d, device="cuda")
+    vm = torch.empty(B, d, device="cuda")
+    check(lib.cmve_mha_absorbed(engine.handle(yc.device), engine._ptr(yc), yc.stride(0), d, npix, f, gs, B, H, d,
+                                engine._ptr(uc), uc.stride(0), 1e-5, engine._ptr(z), z.stride(0), engine._ptr(vm),
+                                vm.stride(0)), "cmve_mha_absorbed")
+    yd, ud = yc.double().cpu(), uc.double().cpu()
+    p_idx, c_idx = torch.meshgrid(torch.arange(npix), torch.arange(cpr), indexing="ij")
+    perm = (c_idx * npix + p_idx).reshape(-1)  # kernel element e -> original element
+    zr = torch.empty(B, H, d, dtype=torch.float64)
+    vr = torch.empty(B, d, dtype=torch.float64)
+    for qb in range(B):
+        g, bb = divmod(qb, gs)
+        keys = []
+        for t in range(T):
+            R = t * gs + bb
+            bf, run = g * gs * f + R // L, R % L
+            blk = yd[bf * npix:(bf + 1) * npix, run * cpr:(run + 1) * cpr]  # [p, c']
+            keys.append(blk.reshape(-1))  # kernel order e = p*cpr + c'
+        X = torch.stack(keys)  # [T, d] kernel order
+        n = (X - X.mean(1, keepdim=True)) / torch.sqrt(X.var(1, unbiased=False, keepdim=True) + 1e-5)
+        s = n @ ud[qb].view(H, d).T  # [T, H]
+        p = torch.softmax(s, 0)
+        zr[qb] = p.T @ n
+        orig = torch.empty_like(X)
+        orig[:, perm] = X
+        vr[qb] = orig.mean(0)
+    assert (z.double().cpu().view(B, H, d) - zr).abs().max().item() < 2e-5
+    assert (vm.double().cpu() - vr).abs().max().item() < 2e-6

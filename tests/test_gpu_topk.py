@@ -260,3 +260,54 @@ def test_gallery_scorer_resident_buffers(torch_cuda):
         idx = sc.topk_indices(arg, 7)
         expect = np.argsort(R.cal_error(gal, caps), axis=1, kind="stable")[:, :7]
         assert np.array_equal(idx, expect), f"call {t}"
+
+
+@pytest.mark.parametrize("k,nc,ties", [(10, 5000, False), (64, 3000, True), (2048, 9000, True), (7, 5, True)])
+def test_topk_dense_merge_kernel(torch_cuda, k, nc, ties):
+    """K12f (cmve_topk_dense_merge) against numpy's stable sort of the same candidates by (score desc, id asc):
+    a running best of k entries merged with a chunk of fp64 scores (ids j0 + c), exact ties (many rows share
+    the k-th score), NaN (-> -inf, last) and -0.0 (== +0.0); the first chunk (kb = 0) and fewer candidates
+    than k (ids -1 / -inf past them)."""
+    import torch
+    from cmve import engine
+    from cmve._lib import lib, check
+    rng = np.random.default_rng(k + nc)
+    rows = 3
+    s = rng.standard_normal((rows, nc))
+    if ties:
+        s = np.round(s, 1)  # ~60 distinct values: heavy ties at every rank
+        s[:, ::17] = np.nan
+        s[:, 5::23] = -0.0
+        s[:, 6::23] = 0.0
+    st = torch.from_numpy(s).cuda()
+
+    def run(best_s, best_i, kb, chunk, j0):
+        out_s = torch.empty((rows, k), dtype=torch.float64, device="cuda")
+        out_i = torch.empty((rows, k), dtype=torch.int64, device="cuda")
+        check(lib.cmve_topk_dense_merge(engine.handle(st.device), engine._ptr(best_s), engine._ptr(best_i), kb,
+                                        engine._ptr(chunk), chunk.stride(0), rows, chunk.shape[1], j0, k,
+                                        engine._ptr(out_s), engine._ptr(out_i)), "cmve_topk_dense_merge")
+        return out_s.cpu().numpy(), out_i.cpu().numpy()
+
+    def ref(vals, ids):
+        v = np.where(np.isnan(vals), -np.inf, vals)
+        o = np.lexsort((ids, -v))  # primary: score desc, then id asc
+        return v[o][:k], ids[o][:k]
+
+    # first chunk (no running best), then a second chunk merged with it
+    h = nc // 2
+    empty_s = torch.empty((rows, 1), dtype=torch.float64, device="cuda")
+    empty_i = torch.empty((rows, 1), dtype=torch.int64, device="cuda")
+    b_s, b_i = run(empty_s, empty_i, 0, st[:, :h].contiguous(), 0)
+    kb = min(k, h)
+    bs_t = torch.from_numpy(np.ascontiguousarray(b_s[:, :kb])).cuda()
+    bi_t = torch.from_numpy(np.ascontiguousarray(b_i[:, :kb])).cuda()
+    m_s, m_i = run(bs_t, bi_t, kb, st[:, h:].contiguous(), h)
+    for r in range(rows):
+        e_s, e_i = ref(s[r, :h], np.arange(h))
+        n1 = len(e_i)
+        assert np.array_equal(b_i[r, :n1], e_i) and np.array_equal(b_s[r, :n1], e_s)
+        assert np.all(b_i[r, n1:] == -1)
+        e_s, e_i = ref(s[r], np.arange(nc))
+        n2 = len(e_i)
+        assert np.array_equal(m_i[r, :n2], e_i) and np.array_equal(m_s[r, :n2], e_s)
