@@ -587,6 +587,76 @@ class RankSession:
         return t2v, v2t
 
 
+class RankBatch:
+    """A batch of same-shaped RankSession evaluations (cmve_eval_batch_*: one prep, one rank GEMM and one
+    finish launch over all of them).  ``sessions`` share sizes, dtype, mode and GT lists (each keeps its own
+    packed sets, workspace and output); ``inputs`` holds one (captions, videos) pair of device tensors of the
+    session dtype per session, read in place (refill them between runs: every address is baked in, as for
+    RankSession.graph); ``outs`` optionally one int64 output per session (default each session's ``out``).
+    ``run()`` enqueues the batch on ``stream`` (default the current stream); the results equal each session's
+    own ``enqueue`` bit for bit.  Sizes must take the G64 rank geometry (e.g. MSR-VTT-1kA's 1,000 x 1,000)."""
+
+    def __init__(self, sessions, inputs, outs=None, stream: Optional["torch.cuda.Stream"] = None):
+        sessions = list(sessions)
+        if not sessions or len(inputs) != len(sessions):
+            raise ValueError("RankBatch: one (captions, videos) input pair per session")
+        s0 = sessions[0]
+        for s in sessions[1:]:
+            same_lists = all((a is None) == (b is None) and (a is None or all(torch.equal(x, y) for x, y in zip(a, b)))
+                             for a, b in ((s0.row, s.row), (s0.col, s.col)))
+            if (s.q.n, s.g.n, s.q.d, s.dtype, s.mode, s.paired) != (s0.q.n, s0.g.n, s0.q.d, s0.dtype, s0.mode,
+                                                                   s0.paired) or not same_lists:
+                raise ValueError("RankBatch: sessions must share sizes, dtype, mode and GT lists")
+        outs = [s.out for s in sessions] if outs is None else list(outs)
+        for s, o in zip(sessions, outs):
+            if o.dtype != torch.int64 or not o.is_contiguous() or o.numel() < s.out.numel():
+                raise ValueError("RankBatch: outs must be contiguous int64 tensors of EVAL_OUT_HEAD + n_q + n_g words")
+        for s, (c, v) in zip(sessions, inputs):
+            for x in (c, v):
+                if not (torch.is_tensor(x) and x.device == s.device and x.dtype == s.dtype):
+                    raise ValueError("RankBatch: inputs must be device tensors of the session dtype")
+            s.enqueue(c, v, _bind_only=True)
+            if s._bound[0] is not c or s._bound[1] is not v:
+                raise ValueError("RankBatch: inputs must be readable in place (rows contiguous)")
+        n = len(sessions)
+        self._q = (C.POINTER(Rows) * n)(*[C.pointer(s.q.desc) for s in sessions])
+        self._g = (C.POINTER(Rows) * n)(*[C.pointer(s.g.desc) for s in sessions])
+        self._ws = (C.c_void_p * n)(*[s.ws.data_ptr() for s in sessions])
+        self._out = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        ws_bytes = min(s.ws.numel() for s in sessions)
+        cap = min(s.cap for s in sessions)
+        r = s0.row if s0.row is not None else (None, None)
+        c = s0.col if s0.col is not None else (None, None)
+        mode = s0.mode | (_lib.EVAL_PAIRED if s0.paired else 0)
+        bh = C.c_void_p()
+        check(lib.cmve_eval_batch_create(n, self._q, self._g, mode, _ptr(r[0]), _ptr(r[1]), _ptr(c[0]), _ptr(c[1]),
+                                         self._ws, ws_bytes, cap, self._out, C.byref(bh)), "cmve_eval_batch_create")
+        self._b = bh.value
+        self._keep = (sessions, [tuple(x) for x in inputs], outs)  # everything the table points at stays alive
+        self._ws_gens = [s._ws_gen for s in sessions]
+        self.sessions, self.outs, self.stream = sessions, outs, stream
+        self._h = stream_handle(s0.device, stream) if stream is not None else None
+
+    def run(self):
+        if not self._b:
+            raise RuntimeError("RankBatch.run: the batch was closed")
+        if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
+            raise RuntimeError("RankBatch.run: a session's workspace was regrown after the batch was built")
+        h = self._h if self._h is not None else handle(self.sessions[0].device)
+        check(lib.cmve_eval_batch_run(h, self._b), "cmve_eval_batch_run")
+
+    def close(self):
+        if self._b:
+            lib.cmve_eval_batch_destroy(self._b)
+            self._b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter teardown)
+            pass
+
+
 class EvalGraph:
     """A captured RankSession evaluation (cmve_eval_graph_*): ``launch()`` enqueues it on the session's
     stream with one host call.  Keeps its inputs, output and session alive."""

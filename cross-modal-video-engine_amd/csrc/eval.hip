@@ -286,7 +286,7 @@ constexpr int PREP_NT = CMVE_PREP_NT;  // 4 rows per block: a 1k-A evaluation's 
 constexpr int PREP_NW = PREP_NT / 64;
 
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__device__ __forceinline__ void eval_prep_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
   EVAL_STAMP(c, 0, 0);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide
 // code, and the GT score fma(v, w) chain is symmetric in the two rows.  Padding rows i >= n of both sides
 // are this wave's too (q.n == g.n, q.n_pad == g.n_pad).
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
   EVAL_STAMP(c, 0, 0);
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
@@ -468,7 +468,7 @@ __device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide
 // The ranks of both directions (cmve_gt_ranks' rules) for this block's 256 rows of each side and, per
 // direction, #rank<=1, <=5, <=10 and the rank sum, added into the stats head (zeroed by the prep)
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
   EVAL_STAMP(c, 1, 0);
   if (c.dbg & 32) return;
   __shared__ unsigned long long red[9 * FIN_NW];
@@ -520,6 +520,66 @@ __global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSid
     if ((k < 4 ? q.off : g.off) && a) atomicAdd((unsigned long long*)&c.stats[k], a);
   }
   EVAL_STAMP(c, 1, 1);
+}
+
+// entry kernels: one evaluation (arguments by value), or a batch of same-shaped evaluations whose argument
+// blocks sit in a device table (cmve_eval_batch_*: blockIdx.y = the evaluation; the bodies index blocks by x)
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(PREP_NT) void eval_prep_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  eval_prep_body<TQ, TG>(q, g, c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  eval_prep_pair_body<TQ, TG>(q, g, c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  eval_finish_body<TQ, TG>(q, g, c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(PREP_NT) void eval_prep_batch_kernel(const EvalItem* __restrict__ tab) {
+  const EvalItem& it = tab[blockIdx.y];
+  eval_prep_body<TQ, TG>(it.q, it.g, it.c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(PREP_NT) void eval_prep_pair_batch_kernel(const EvalItem* __restrict__ tab) {
+  const EvalItem& it = tab[blockIdx.y];
+  eval_prep_pair_body<TQ, TG>(it.q, it.g, it.c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(FIN_NT) void eval_finish_batch_kernel(const EvalItem* __restrict__ tab) {
+  const EvalItem& it = tab[blockIdx.y];
+  eval_finish_body<TQ, TG>(it.q, it.g, it.c);
+}
+
+template <typename TQ, typename TG>
+static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int phase,
+                                   hipStream_t s) {
+  if (phase == 0) {
+    const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
+    hipLaunchKernelGGL((eval_prep_batch_kernel<TQ, TG>), dim3(blocks, (unsigned)count), dim3(PREP_NT), 0, s, tab);
+    return check_launch("eval_prep_batch_kernel");
+  }
+  if (phase == 3) {
+    const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);
+    hipLaunchKernelGGL((eval_prep_pair_batch_kernel<TQ, TG>), dim3(blocks, (unsigned)count), dim3(PREP_NT), 0, s,
+                       tab);
+    return check_launch("eval_prep_pair_batch_kernel");
+  }
+  const int64_t nmax = q.n > g.n ? q.n : g.n;
+  hipLaunchKernelGGL((eval_finish_batch_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2,
+                     (unsigned)count), dim3(FIN_NT), 0, s, tab);
+  return check_launch("eval_finish_batch_kernel");
+}
+
+// a batch: the items share q / g shapes, dtypes and GT lists (tab[i] differ in buffers only); phases 0 / 2 / 3
+// as launch_eval (no separate fix-up: the batch path is the G64 inline fix-up geometry)
+int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int q_f64, int g_f64,
+                      int phase, hipStream_t s) {
+  if (!q_f64 && !g_f64) return launch_eval_batch_typed<float, float>(q, g, tab, count, phase, s);
+  if (!q_f64 && g_f64) return launch_eval_batch_typed<float, double>(q, g, tab, count, phase, s);
+  if (q_f64 && !g_f64) return launch_eval_batch_typed<double, float>(q, g, tab, count, phase, s);
+  return launch_eval_batch_typed<double, double>(q, g, tab, count, phase, s);
 }
 
 template <typename TQ, typename TG>

@@ -56,5 +56,12 @@ struct EvalCommon {
   (cp).stamps[((size_t)(kern) * 1024 + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s);
+// one evaluation's argument blocks in a batch's device table (cmve_eval_batch_*)
+struct EvalItem {
+  EvalSide q, g;
+  EvalCommon c;
+};
+int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int q_f64, int g_f64,
+                      int phase, hipStream_t s);
 
 }  // namespace cmve

@@ -19,6 +19,8 @@
 // swizzle applied to the GLOBAL source chunk (chunk ^ (row & 7)) and the matching
 // ds_read_b128 address.  Grid: XCD-aware -- each XCD gets a contiguous range of the logical
 // tile order, which walks 8 gallery tiles x all query tiles.
+#include <vector>
+
 #include "cmve_internal.h"
 
 namespace cmve {
@@ -291,8 +293,12 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_G64_BLOCKS
 #define CMVE_G64_BLOCKS 2
 #endif
-template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
-__global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2) void sim_kernel(SimArgs a) {
+// BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): blockIdx.y picks the problem's
+// argument block in `tab` (the tile walk indexes blocks by x only); otherwise `tab` is unused
+template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
+__global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2) void sim_kernel(
+    SimArgs a_arg, const SimArgs* __restrict__ tab) {
+  const SimArgs a = BATCH ? tab[blockIdx.y] : a_arg;
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -307,6 +313,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
   // ... (same XCD, same XCD-local order as a one-tile-per-block grid); the G128 grid is one tile each
   const int ntiles = a.nblk_m * a.nblk_n;
   int tile = blockIdx.x;
+  if (tile >= ntiles) return;  // (a grid / argument mismatch ends here instead of in a wild tile walk)
   int m0, n0;
   auto tile_origin = [&](int t, int& mo, int& no) {
     int bm_, bn_;
@@ -1259,6 +1266,17 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
   if constexpr (!PHASED) epilogue();
 }
 
+// the launch geometry's fields of SimArgs: tile grid and the tile-order group width
+static void geo_fill(SimArgs& a, int64_t nq_pad, int64_t ng_pad, int bm, int bn) {
+  a.nblk_m = (int)(nq_pad / bm);
+  a.nblk_n = (int)(ng_pad / bn);
+  static const int gn_env = [] {
+    const char* e = getenv("CMVE_SIM_GN");  // kernel studies only
+    return e ? atoi(e) : 0;
+  }();
+  a.gn = gn_env > 0 ? gn_env : 8;
+}
+
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
@@ -1268,19 +1286,14 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
   static const hipError_t attr_err = hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   CMVE_HIP(attr_err);
-  a.nblk_m = (int)(nq_pad / G::BM);
-  a.nblk_n = (int)(ng_pad / G::BN);
-  static const int gn_env = [] {
-    const char* e = getenv("CMVE_SIM_GN");  // kernel studies only
-    return e ? atoi(e) : 0;
-  }();
-  a.gn = gn_env > 0 ? gn_env : 8;
+  geo_fill(a, nq_pad, ng_pad, G::BM, G::BN);
   unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
   if constexpr (PHASED) {  // persistent: one block per CU (a multiple of 8: the XCD map is blockIdx & 7)
     const int cus = std::max(8, device_cus() / 8 * 8);
     nblocks = std::min<unsigned>(nblocks, (unsigned)cus);
   }
-  cmve::launch(sim_kernel<MODE, EPI, WM, WN, TM, PHASED>, dim3(nblocks), dim3(G::NT), (uint32_t)lds, stream, a);
+  cmve::launch(sim_kernel<MODE, EPI, WM, WN, TM, PHASED>, dim3(nblocks), dim3(G::NT), (uint32_t)lds, stream, a,
+               (const SimArgs*)nullptr);
   return check_launch("sim_kernel");
 }
 
@@ -1747,34 +1760,42 @@ __global__ __launch_bounds__(256) void eval_thr_kernel(EvalThrSide s0, EvalThrSi
   s.lo[r] = sgt < INFINITY ? f32_round_down(sgt - E) : INFINITY;
 }
 
-extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags,
-                               const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
-                               const int32_t* col_idx, void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out,
-                               int32_t timing_slot) {
-  CMVE_REQUIRE(h, "cmve_eval_ranks: NULL handle");
+// Everything of one K14 evaluation but its launches: argument checks, the workspace layout and the argument
+// blocks of the prep / rank GEMM / fix-up / finish launches (cmve_eval_ranks launches them at once;
+// cmve_eval_batch_create stores them in a device table)
+struct EvalPlan {
+  cmve::EvalSide sq, sg;
+  cmve::EvalCommon c;
+  SimArgs a;
+  int qf, gf;
+  bool paired, inline_fix;
+};
+
+static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, const int64_t* row_off,
+                        const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx, void* ws,
+                        int64_t ws_bytes, int64_t cand_cap, int64_t* out, const char* fn, EvalPlan& P) {
   const int32_t mode = mode_flags & 0xff;
   const bool paired_req = (mode_flags & CMVE_EVAL_PAIRED) != 0;
-  CMVE_REQUIRE((mode_flags & ~(0xff | CMVE_EVAL_PAIRED)) == 0, "cmve_eval_ranks: unknown flags 0x%x", mode_flags);
-  int st = validate_pair(q, g, mode, "cmve_eval_ranks");
+  CMVE_REQUIRE((mode_flags & ~(0xff | CMVE_EVAL_PAIRED)) == 0, "%s: unknown flags 0x%x", fn, mode_flags);
+  int st = validate_pair(q, g, mode, fn);
   if (st) return st;
-  CMVE_REQUIRE(q->n > 0 && g->n > 0, "cmve_eval_ranks: both sets need rows");
+  CMVE_REQUIRE(q->n > 0 && g->n > 0, "%s: both sets need rows", fn);
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm && q->err_hi && q->err_hilo && g->err_hi &&
                    g->err_hilo && q->err_max && g->err_max,
-               "cmve_eval_ranks: packed-set arrays missing");
-  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "cmve_eval_ranks: sets packed CMVE_PACK_RAW have no score bound");
+               "%s: packed-set arrays missing", fn);
+  CMVE_REQUIRE(!((q->flags | g->flags) & CMVE_PACK_RAW), "%s: sets packed CMVE_PACK_RAW have no score bound", fn);
   CMVE_REQUIRE((q->raw_dtype == CMVE_F32 || q->raw_dtype == CMVE_F64) &&
                    (g->raw_dtype == CMVE_F32 || g->raw_dtype == CMVE_F64),
-               "cmve_eval_ranks: raw rows must be F32 or F64");
-  CMVE_REQUIRE(q->raw_ld >= q->d && g->raw_ld >= g->d, "cmve_eval_ranks: raw_ld < d");
+               "%s: raw rows must be F32 or F64", fn);
+  CMVE_REQUIRE(q->raw_ld >= q->d && g->raw_ld >= g->d, "%s: raw_ld < d", fn);
   CMVE_REQUIRE((q->h16 == nullptr) == (q->err_h16 == nullptr) && (g->h16 == nullptr) == (g->err_h16 == nullptr),
-               "cmve_eval_ranks: h16 and err_h16 go together");
+               "%s: h16 and err_h16 go together", fn);
   CMVE_REQUIRE((row_off != nullptr) == (row_idx != nullptr) && (col_off != nullptr) == (col_idx != nullptr),
-               "cmve_eval_ranks: GT offsets and indices go together");
-  CMVE_REQUIRE(row_off || col_off, "cmve_eval_ranks: no direction requested");
-  CMVE_REQUIRE(ws && out, "cmve_eval_ranks: NULL workspace / output");
-  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_ranks: bad timing slot");
+               "%s: GT offsets and indices go together", fn);
+  CMVE_REQUIRE(row_off || col_off, "%s: no direction requested", fn);
+  CMVE_REQUIRE(ws && out, "%s: NULL workspace / output", fn);
   const EvalWs w = eval_ws_layout(q->n_pad, g->n_pad, cand_cap);
-  CMVE_REQUIRE(cand_cap > 0 && ws_bytes >= (int64_t)w.total, "cmve_eval_ranks: workspace has %lld bytes, needs %lld",
+  CMVE_REQUIRE(cand_cap > 0 && ws_bytes >= (int64_t)w.total, "%s: workspace has %lld bytes, needs %lld", fn,
                (long long)ws_bytes, (long long)w.total);
   CandLayout l = cand_layout(g->n_pad, cand_cap);
   // one bucket per 64 x 64 output tile when the grid is small: each wave reserves its undecided-pair
@@ -1786,29 +1807,16 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     l.nb = nb_tiles;
     l.cap_b = (cand_cap - nb_tiles) / nb_tiles;
   }
-  CMVE_REQUIRE(l.cap_b > 0, "cmve_eval_ranks: cand_cap %lld cannot hold the %lld bucket counters", (long long)cand_cap,
+  CMVE_REQUIRE(l.cap_b > 0, "%s: cand_cap %lld cannot hold the %lld bucket counters", fn, (long long)cand_cap,
                (long long)l.nb);
-  CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "cmve_eval_ranks: gallery set too large (%lld buckets)",
+  CMVE_REQUIRE((l.nb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD, "%s: gallery set too large (%lld buckets)", fn,
                (long long)l.nb);
-  hipEvent_t* ev = nullptr;
-  hipEvent_t* kev = nullptr;
-  if (timing_slot >= 0) {
-    ev = h->eval_ev[timing_slot];
-    for (int k = 0; k < 4; ++k)
-      if (!ev[k]) CMVE_HIP(hipEventCreate(&ev[k]));
-    kev = h->eval_kev[timing_slot];
-    for (int k = 0; k < 8; ++k)
-      if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
-  }
-  auto arm = [&](int k) {  // the next launch's own start / stop (cmve::launch)
-    if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
-  };
   char* base = (char*)ws;
-  cmve::EvalSide sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, w.q_gt1,
-                                out + CMVE_EVAL_OUT_HEAD);
-  cmve::EvalSide sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt, w.g_gt1,
-                                out + CMVE_EVAL_OUT_HEAD + q->n);
-  cmve::EvalCommon c{};
+  P.sq = eval_side(q, row_off, row_idx, base, w.q_sgt, w.q_hi, w.q_lo, w.q_cnt, w.q_gt1, out + CMVE_EVAL_OUT_HEAD);
+  P.sg = eval_side(g, col_off, col_idx, base, w.g_sgt, w.g_hi, w.g_lo, w.g_cnt, w.g_gt1,
+                   out + CMVE_EVAL_OUT_HEAD + q->n);
+  cmve::EvalCommon& c = P.c;
+  c = cmve::EvalCommon{};
   c.d = q->d;
   c.d_pad = q->d_pad;
   c.mode = mode;
@@ -1831,19 +1839,15 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   }
   c.stamps = (dbg & 128) ? stamp_buf : nullptr;
   g_eval_stamps = c.stamps;
-  const int qf = q->raw_dtype == CMVE_F64, gf = g->raw_dtype == CMVE_F64;
+  P.qf = q->raw_dtype == CMVE_F64;
+  P.gf = g->raw_dtype == CMVE_F64;
   if (paired_req)
     CMVE_REQUIRE(row_off && col_off && q->n == g->n && q->n_pad == g->n_pad,
-                 "cmve_eval_ranks: CMVE_EVAL_PAIRED needs both directions and equal set sizes");
+                 "%s: CMVE_EVAL_PAIRED needs both directions and equal set sizes", fn);
   // the paired prep reads rows through the register path only (16-B pieces, d_pad <= 1024)
-  const bool paired = paired_req && sq.vec && sg.vec && q->d_pad <= 1024;
-  hipStream_t s = h->stream;
-  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
-  arm(0);
-  st = cmve::launch_eval(sq, sg, c, qf, gf, paired ? 3 : 0, s);
-  if (st) return st;
-  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
-  SimArgs a = make_args(q, g, mode);
+  P.paired = paired_req && P.sq.vec && P.sg.vec && q->d_pad <= 1024;
+  SimArgs& a = P.a;
+  a = make_args(q, g, mode);
   // thresholds derived in the GEMM from the prep's GT scores and per-row bounds (row_hi / col_hi only
   // mark the directions that are on)
   a.thr_gt = !sim_uses_phased(mode, q->n_pad, g->n_pad);
@@ -1852,16 +1856,16 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   a.q_emax = c.emax + (0 * 3 + mode_slot(mode)) * cmve::EMAX_SHARDS;
   a.g_emax = c.emax + (1 * 3 + mode_slot(mode)) * cmve::EMAX_SHARDS;
   if (row_off) {
-    a.row_hi = sq.thr_hi;
-    a.row_lo = sq.thr_lo;
-    a.row_sgt = sq.sgt;
-    a.row_cnt = sq.cnt;
+    a.row_hi = P.sq.thr_hi;
+    a.row_lo = P.sq.thr_lo;
+    a.row_sgt = P.sq.sgt;
+    a.row_cnt = P.sq.cnt;
   }
   if (col_off) {
-    a.col_hi = sg.thr_hi;
-    a.col_lo = sg.thr_lo;
-    a.col_sgt = sg.sgt;
-    a.col_cnt = sg.cnt;
+    a.col_hi = P.sg.thr_hi;
+    a.col_lo = P.sg.thr_lo;
+    a.col_sgt = P.sg.sgt;
+    a.col_cnt = P.sg.cnt;
   }
   set_cand(a, g, cand, cand_cap, out + 10);  // (the epilogue never writes cand_count)
   a.bucket_cnt = (unsigned long long*)cand;  // the evaluation's layout (l: per-tile buckets when small)
@@ -1870,17 +1874,17 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   a.tile_buckets = tile_buckets;
   a.nbn64 = (int)(g->n_pad >> 6);
   if (a.thr_gt) {  // (the 2-stage / ring kernels; the persistent G256 kernel keeps every undecided pair)
-    a.row_gt1 = sq.gt1;
-    a.col_gt1 = sg.gt1;
+    a.row_gt1 = P.sq.gt1;
+    a.col_gt1 = P.sg.gt1;
   }
   // G64 (1k-A scale): the rank GEMM re-scores its own undecided pairs (no list, no fix-up launch)
   const char* fix_env = getenv("CMVE_EVAL_FIX_LAUNCH");  // kernel studies / tests: the separate fix-up launch
   const bool no_inline = fix_env && atoi(fix_env) != 0;
-  const bool inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
-  if (inline_fix) {
+  P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
+  if (P.inline_fix) {
     a.fix_inline = 1;
-    a.q_f64 = qf;
-    a.g_f64 = gf;
+    a.q_f64 = P.qf;
+    a.g_f64 = P.gf;
     a.q_raw = q->raw;
     a.g_raw = g->raw;
     a.q_ld = q->raw_ld;
@@ -1891,9 +1895,43 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
     c.fix_inline = 1;
   }
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags,
+                               const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
+                               const int32_t* col_idx, void* ws, int64_t ws_bytes, int64_t cand_cap, int64_t* out,
+                               int32_t timing_slot) {
+  CMVE_REQUIRE(h, "cmve_eval_ranks: NULL handle");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_ranks: bad timing slot");
+  EvalPlan P;
+  int st = eval_prepare(q, g, mode_flags, row_off, row_idx, col_off, col_idx, ws, ws_bytes, cand_cap, out,
+                        "cmve_eval_ranks", P);
+  if (st) return st;
+  const int32_t mode = mode_flags & 0xff;
+  hipEvent_t* ev = nullptr;
+  hipEvent_t* kev = nullptr;
+  if (timing_slot >= 0) {
+    ev = h->eval_ev[timing_slot];
+    for (int k = 0; k < 4; ++k)
+      if (!ev[k]) CMVE_HIP(hipEventCreate(&ev[k]));
+    kev = h->eval_kev[timing_slot];
+    for (int k = 0; k < 8; ++k)
+      if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
+  }
+  auto arm = [&](int k) {  // the next launch's own start / stop (cmve::launch)
+    if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
+  };
+  hipStream_t s = h->stream;
+  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
+  arm(0);
+  st = cmve::launch_eval(P.sq, P.sg, P.c, P.qf, P.gf, P.paired ? 3 : 0, s);
+  if (st) return st;
+  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
+  const SimArgs& a = P.a;
   if (!a.thr_gt) {
-    EvalThrSide t0{a.row_sgt, a.q_err, a.g_emax, row_off ? sq.thr_hi : nullptr, sq.thr_lo, q->n_pad};
-    EvalThrSide t1{a.col_sgt, a.g_err, a.q_emax, col_off ? sg.thr_hi : nullptr, sg.thr_lo, g->n_pad};
+    EvalThrSide t0{a.row_sgt, a.q_err, a.g_emax, row_off ? P.sq.thr_hi : nullptr, P.sq.thr_lo, q->n_pad};
+    EvalThrSide t1{a.col_sgt, a.g_err, a.q_emax, col_off ? P.sg.thr_hi : nullptr, P.sg.thr_lo, g->n_pad};
     const int64_t nthr = q->n_pad + g->n_pad;
     hipLaunchKernelGGL(eval_thr_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, t0, t1, q->d_pad,
                        (int)mode);
@@ -1904,16 +1942,126 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = inline_fix;
-  if (!inline_fix) {
+  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = P.inline_fix;
+  if (!P.inline_fix) {
     arm(2);
-    st = cmve::launch_eval(sq, sg, c, qf, gf, 1, s);
+    st = cmve::launch_eval(P.sq, P.sg, P.c, P.qf, P.gf, 1, s);
     if (st) return st;
   }
   arm(3);
-  st = cmve::launch_eval(sq, sg, c, qf, gf, 2, s);
+  st = cmve::launch_eval(P.sq, P.sg, P.c, P.qf, P.gf, 2, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
+  return CMVE_OK;
+}
+
+// ---- K14 batches: same-shaped evaluations (MSR-VTT-1kA-sized, the G64 inline fix-up geometry) in ONE set of
+// three launches, each with a grid of (blocks of one evaluation) x (evaluations): a 1k x 1k evaluation's
+// launches leave most of the chip idle, a batch fills it (every launch's argument blocks in a device table).
+struct cmve_eval_batch {
+  int count = 0;
+  int qf = 0, gf = 0, mode = 0;
+  bool paired = false;
+  int64_t nq_pad = 0, ng_pad = 0;
+  cmve::EvalSide sq0, sg0;        // the shapes (the launch grids)
+  cmve::EvalItem* d_items = nullptr;
+  SimArgs* d_args = nullptr;
+};
+
+template <int MODE>
+static int launch_rank_batch(const SimArgs& a0, const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
+                             hipStream_t stream) {
+  using G = Geo<4, 1, 1>;
+  const size_t lds = ring_stages<MODE, G::BM, G::BN, false>() * stage_bytes<MODE, G::BM, G::BN, false>();
+  static const hipError_t attr_err = hipFuncSetAttribute(
+      (const void*)sim_kernel<MODE, EPI_RANK, 4, 1, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)lds);
+  CMVE_HIP(attr_err);
+  const unsigned nblocks = (unsigned)((nq_pad / G::BM) * (ng_pad / G::BN));
+  hipLaunchKernelGGL((sim_kernel<MODE, EPI_RANK, 4, 1, 1, false, true>), dim3(nblocks, (unsigned)count),
+                     dim3(G::NT), (uint32_t)lds, stream, a0, tab);
+  return check_launch("sim_kernel (batch)");
+}
+
+extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* const* g,
+                                      int32_t mode_flags, const int64_t* row_off, const int32_t* row_idx,
+                                      const int64_t* col_off, const int32_t* col_idx, void* const* ws,
+                                      int64_t ws_bytes, int64_t cand_cap, int64_t* const* out,
+                                      cmve_eval_batch_t* batch) {
+  CMVE_REQUIRE(batch && q && g && ws && out && count >= 1 && count <= 65535,
+               "cmve_eval_batch_create: NULL argument / count out of [1, 65535]");
+  *batch = nullptr;
+  std::vector<cmve::EvalItem> items((size_t)count);
+  std::vector<SimArgs> args((size_t)count);
+  EvalPlan P0;
+  for (int i = 0; i < count; ++i) {
+    EvalPlan P;
+    const int st = eval_prepare(q[i], g[i], mode_flags, row_off, row_idx, col_off, col_idx, ws[i], ws_bytes,
+                                cand_cap, out[i], "cmve_eval_batch_create", P);
+    if (st) return st;
+    CMVE_REQUIRE(P.inline_fix, "cmve_eval_batch_create: batches take the G64 geometry (fewer than 128 tiles of "
+                               "128^2, e.g. 1,000 x 1,000) with the inline fix-up");
+    CMVE_REQUIRE(P.c.stamps == nullptr, "cmve_eval_batch_create: CMVE_EVAL_DBG stamps are per evaluation");
+    if (i == 0) {
+      P0 = P;
+    } else {
+      CMVE_REQUIRE(q[i]->n == q[0]->n && g[i]->n == g[0]->n && q[i]->n_pad == q[0]->n_pad &&
+                       g[i]->n_pad == g[0]->n_pad && q[i]->d == q[0]->d && q[i]->d_pad == q[0]->d_pad &&
+                       P.qf == P0.qf && P.gf == P0.gf && P.paired == P0.paired,
+                   "cmve_eval_batch_create: evaluation %d differs in shape / dtype / pairing from the first", i);
+      for (int j = 0; j < i; ++j)
+        CMVE_REQUIRE(ws[j] != ws[i] && out[j] != out[i],
+                     "cmve_eval_batch_create: evaluations %d and %d share a workspace or an output", j, i);
+    }
+    items[(size_t)i] = cmve::EvalItem{P.sq, P.sg, P.c};
+    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, 64, 64);  // (launch_geo fills these for a single launch)
+    args[(size_t)i] = P.a;
+  }
+  auto* b = new cmve_eval_batch;
+  b->count = count;
+  b->qf = P0.qf;
+  b->gf = P0.gf;
+  b->mode = mode_flags & 0xff;
+  b->paired = P0.paired;
+  b->nq_pad = q[0]->n_pad;
+  b->ng_pad = g[0]->n_pad;
+  b->sq0 = P0.sq;
+  b->sg0 = P0.sg;
+  hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
+  if (e == hipSuccess) e = hipMalloc(&b->d_args, sizeof(SimArgs) * (size_t)count);
+  if (e == hipSuccess)
+    e = hipMemcpy(b->d_items, items.data(), sizeof(cmve::EvalItem) * (size_t)count, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b->d_args, args.data(), sizeof(SimArgs) * (size_t)count, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(b->d_items);
+    (void)hipFree(b->d_args);
+    delete b;
+    CMVE_HIP(e);
+  }
+  *batch = b;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b) {
+  CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
+  hipStream_t s = h->stream;
+  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
+  if (st) return st;
+  SimArgs a0{};  // (the by-value argument is unused by the batched kernel)
+  switch (b->mode) {
+    case CMVE_SIM_F16: st = launch_rank_batch<CMVE_SIM_F16>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
+    case CMVE_SIM_BF16: st = launch_rank_batch<CMVE_SIM_BF16>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
+    default: st = launch_rank_batch<CMVE_SIM_BF16X3>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
+  }
+  if (st) return st;
+  return cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, 2, s);
+}
+
+extern "C" int cmve_eval_batch_destroy(cmve_eval_batch_t b) {
+  if (!b) return CMVE_OK;
+  (void)hipFree(b->d_items);
+  (void)hipFree(b->d_args);
+  delete b;
   return CMVE_OK;
 }
 

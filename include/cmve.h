@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 15
+#define CMVE_ABI_VERSION 16
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -419,6 +419,21 @@ int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
  * stream into a HIP graph; every pointer and size is baked in, so q->raw / g->raw, the GT lists, ws and
  * out must stay at their addresses.  launch replays it on h's stream with one host call (same results
  * bit for bit); destroy frees it. */
+/* K14 batches: `count` same-shaped evaluations (the same q / g sizes, dtypes, mode and GT lists; each its own
+ * packed sets, workspace and output, as for cmve_eval_ranks) run as ONE prep, ONE rank GEMM and ONE finish
+ * launch, each over (the blocks of one evaluation) x (the evaluations): a 1,000 x 1,000 evaluation's launches
+ * leave most of the chip idle, a batch fills it.  The argument blocks are built and copied to the device at
+ * create time (every pointer is baked in: refill the raw rows in place between runs, as for the graph form);
+ * run enqueues the three launches on h's stream; the results equal cmve_eval_ranks' bit for bit.  Batches take
+ * the G64 geometry (fewer than 128 tiles of 128^2) with the rank GEMM's inline fp64 re-score (no overflow).
+ * create synchronises (it uploads the table). */
+typedef struct cmve_eval_batch* cmve_eval_batch_t;
+int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* const* g, int32_t mode,
+                           const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
+                           const int32_t* col_idx, void* const* ws, int64_t ws_bytes, int64_t cand_cap,
+                           int64_t* const* out, cmve_eval_batch_t* batch);
+int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch);
+int cmve_eval_batch_destroy(cmve_eval_batch_t batch);
 typedef struct cmve_eval_graph* cmve_eval_graph_t;
 int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,
                            const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,

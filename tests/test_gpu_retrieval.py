@@ -736,3 +736,57 @@ def test_paired_prep_equals_general_prep(torch_cuda, dt):
         s = R.exact_scores64(ct.double().cpu().numpy(), vt.double().cpu().numpy())
     assert np.array_equal(r1, R.rank_counts(s, t2v)) and np.array_equal(c1, R.rank_counts(s.T, v2t))
     assert r1[3] == n
+
+
+@pytest.mark.parametrize("case", ["c1_paired_f64", "multi_gt_f32"])
+def test_rank_batch_equals_sessions(golden, torch_cuda, case):
+    """RankBatch (cmve_eval_batch_*: one prep, one rank GEMM, one finish launch over several evaluations)
+    against each session's own evaluation of the same inputs: every output word (R@K head, pair total, ranks)
+    equal, the C1 set's ranks equal the reference's; refilled inputs are picked up by the next run."""
+    import torch
+    from cmve import engine
+    if case == "c1_paired_f64":
+        v, c, vid, cid = _c1()
+        v2t_gt, t2v_gt = R.get_gt(vid, cid)
+        rows, cols = [t2v_gt[i] for i in range(len(cid))], v2t_gt
+        dt, sets = torch.float64, []
+        rng = np.random.default_rng(5)
+        for j in range(4):
+            cj = c if j == 0 else c + 0.3 * rng.standard_normal(c.shape)
+            sets.append((torch.from_numpy(cj).cuda(), torch.from_numpy(v).cuda()))
+    else:
+        rng = np.random.default_rng(6)
+        nq, ng, d = 700, 900, 384
+        rows = [[int(x) for x in rng.choice(ng, size=1 + i % 3, replace=False)] for i in range(nq)]
+        cols = [[] for _ in range(ng)]
+        for i, l in enumerate(rows):
+            for j in l:
+                cols[j].append(i)
+        dt, sets = torch.float32, []
+        for j in range(3):
+            gal = rng.standard_normal((ng, d)).astype(np.float32)
+            qs = (gal[[l[0] for l in rows]] + 0.9 * rng.standard_normal((nq, d))).astype(np.float32)
+            sets.append((torch.from_numpy(qs).cuda(), torch.from_numpy(gal).cuda()))
+    n_q, n_g, d = sets[0][0].shape[0], sets[0][1].shape[0], sets[0][0].shape[1]
+    ref = []
+    for cq, gv in sets:
+        s = engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt)
+        s.run(cq, gv)
+        ref.append(s.out.clone())
+    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt) for _ in sets]
+    b = engine.RankBatch(sess, sets)
+    for _ in range(2):
+        b.run()
+        torch.cuda.synchronize()
+        for s, r in zip(sess, ref):
+            assert torch.equal(s.out, r)
+    if case == "c1_paired_f64":
+        g = golden("retrieval_c1")
+        h = sess[0].out.cpu().numpy()
+        assert np.array_equal(h[16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[16 + n_q:], g["v2t_ranks"])
+    sets[1][0].copy_(sets[2][0])  # refill in place: the next run sees it
+    sets[1][1].copy_(sets[2][1])
+    b.run()
+    torch.cuda.synchronize()
+    assert torch.equal(sess[1].out, ref[2])
+    b.close()
