@@ -82,7 +82,7 @@ SIGNATURES = {
     "cmve_mha_1q": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _i32, _vp, _i64]),
     "cmve_eval_batch_create": (C.c_int, [C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp,
                                          _vp]),
-    "cmve_eval_batch_run": (C.c_int, [_vp, _vp]),
+    "cmve_eval_batch_run": (C.c_int, [_vp, _vp, C.c_int32]),
     "cmve_eval_batch_destroy": (C.c_int, [_vp]),
     "cmve_topk_dense_merge": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp]),
     "cmve_mha_absorbed": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _vp, _i64, _f64,
@@ -156,7 +156,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -637,13 +637,23 @@ class RankBatch:
         self.sessions, self.outs, self.stream = sessions, outs, stream
         self._h = stream_handle(s0.device, stream) if stream is not None else None
 
-    def run(self):
+    def run(self, timing_slot: int = -1):
+        """Enqueue the batch; ``timing_slot`` >= 0 records its launches' durations in that slot of the stream
+        handle's timing ring (``kernel_timing``)."""
         if not self._b:
             raise RuntimeError("RankBatch.run: the batch was closed")
         if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
             raise RuntimeError("RankBatch.run: a session's workspace was regrown after the batch was built")
         h = self._h if self._h is not None else handle(self.sessions[0].device)
-        check(lib.cmve_eval_batch_run(h, self._b), "cmve_eval_batch_run")
+        check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
+
+    def kernel_timing(self, slot: int):
+        """(prep, rank GEMM, 0, finish) durations in ms of the batch run that used `slot` (each launch's own
+        start / stop: the whole batch's launches)."""
+        ms = (C.c_float * 4)()
+        h = self._h if self._h is not None else handle(self.sessions[0].device)
+        check(lib.cmve_eval_kernel_timing(h, int(slot), ms), "cmve_eval_kernel_timing")
+        return list(ms)
 
     def close(self):
         if self._b:

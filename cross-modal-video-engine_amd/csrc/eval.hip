@@ -557,18 +557,17 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
                                    hipStream_t s) {
   if (phase == 0) {
     const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
-    hipLaunchKernelGGL((eval_prep_batch_kernel<TQ, TG>), dim3(blocks, (unsigned)count), dim3(PREP_NT), 0, s, tab);
+    cmve::launch(eval_prep_batch_kernel<TQ, TG>, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
     return check_launch("eval_prep_batch_kernel");
   }
   if (phase == 3) {
     const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);
-    hipLaunchKernelGGL((eval_prep_pair_batch_kernel<TQ, TG>), dim3(blocks, (unsigned)count), dim3(PREP_NT), 0, s,
-                       tab);
+    cmve::launch(eval_prep_pair_batch_kernel<TQ, TG>, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
     return check_launch("eval_prep_pair_batch_kernel");
   }
   const int64_t nmax = q.n > g.n ? q.n : g.n;
-  hipLaunchKernelGGL((eval_finish_batch_kernel<TQ, TG>), dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2,
-                     (unsigned)count), dim3(FIN_NT), 0, s, tab);
+  cmve::launch(eval_finish_batch_kernel<TQ, TG>, dim3((unsigned)((nmax + FIN_NT - 1) / FIN_NT) + 2, (unsigned)count),
+               dim3(FIN_NT), 0u, s, tab);
   return check_launch("eval_finish_batch_kernel");
 }
 

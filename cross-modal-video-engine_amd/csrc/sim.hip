@@ -102,11 +102,17 @@ struct SimArgs {
 };
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
-__device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, int GN, int& bm, int& bn) {
-  const int total = nblk_m * nblk_n;
+// block id -> its XCD's contiguous share of [0, total): XCD x (= bid & 7) walks its own range in dispatch order
+__device__ __forceinline__ int xcd_linear(int bid, int total) {
   const int xcd = bid & 7, local = bid >> 3;
   const int q = total >> 3, r = total & 7;
-  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+__device__ __forceinline__ void tile_grouped(int L, int nblk_m, int nblk_n, int GN, int& bm, int& bn);
+__device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, int GN, int& bm, int& bn) {
+  tile_grouped(xcd_linear(bid, nblk_m * nblk_n), nblk_m, nblk_n, GN, bm, bn);
+}
+__device__ __forceinline__ void tile_grouped(int L, int nblk_m, int nblk_n, int GN, int& bm, int& bn) {
   const int group = L / (GN * nblk_m);
   const int within = L - group * (GN * nblk_m);
   const int gn = min(GN, nblk_n - group * GN);
@@ -229,12 +235,20 @@ constexpr size_t stage_bytes() {
 // (8 per wave per K-tile, ~2.7 us for the first 7 K-tiles of an 8-deep ring in the stamps), so a deeper
 // ring gains nothing alone, while 64 KiB lets two evaluations' rank GEMMs share a CU (two HIP streams:
 // 31.0 -> 26.6 us per evaluation, tools/eval_pipe.py)
-template <int MODE, int BM, int BN, bool PHASED>
+// The 128 x 64 ring (K14 batches only, cmve_eval_batch_*): 3 stages of 24 KiB, so that two blocks still share a CU
+// (2 x (72 KiB + the epilogue scratch) <= 160 KiB)
+template <int MODE, int BM, int BN, bool PHASED, int NW = 4>
 constexpr int ring_stages() {
 #ifndef CMVE_G64_STAGES
 #define CMVE_G64_STAGES 4
 #endif
-  return (PHASED || BM != 64 || BN != 64) ? 2 : CMVE_G64_STAGES;
+#ifndef CMVE_G128R_STAGES
+#define CMVE_G128R_STAGES 3
+#endif
+  // (64 x 64, 128 x 64 and the 8-wave 128 x 128; the 4-wave G128 of mid-size problems keeps its 2-stage loop)
+  return (PHASED || (BN != 64 && !(BM == 128 && BN == 128 && NW == 8)) || (BM != 64 && BM != 128))
+             ? 2
+             : (BM == 64 ? CMVE_G64_STAGES : CMVE_G128R_STAGES);
 }
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
@@ -293,17 +307,30 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_G64_BLOCKS
 #define CMVE_G64_BLOCKS 2
 #endif
-// BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): blockIdx.y picks the problem's
-// argument block in `tab` (the tile walk indexes blocks by x only); otherwise `tab` is unused
+#ifndef CMVE_BATCH_FIX1
+#define CMVE_BATCH_FIX1 1
+#endif
+// BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): the block picks the problem's
+// argument block in `tab` (see batch_item below); otherwise `tab` is unused
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
 __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2) void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
-  const SimArgs a = BATCH ? tab[blockIdx.y] : a_arg;
+  // a batch's blocks: the (evaluation, tile) pairs in evaluation-major order, cut into 8 contiguous ranges, one per
+  // XCD -- an XCD works through one or two evaluations at a time (a 1k-A evaluation's fp16 planes are 4 MB, its
+  // L2's size), not a slice of every evaluation in flight (L2 hit rate 61% that way)
+  int batch_item = 0, batch_tile = 0;
+  if constexpr (BATCH) {
+    const int per = (int)gridDim.x;
+    const int L = xcd_linear((int)(blockIdx.y * gridDim.x + blockIdx.x), per * (int)gridDim.y);
+    batch_item = L / per;
+    batch_tile = L - batch_item * per;
+  }
+  const SimArgs a = BATCH ? tab[batch_item] : a_arg;
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED>();
-  constexpr int NS = ring_stages<MODE, BM, BN, PHASED>();
+  constexpr int NS = ring_stages<MODE, BM, BN, PHASED, NW>();
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -312,12 +339,13 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
   // tiles: the phased (G256) kernel is persistent -- one block per CU walks tile, tile + gridDim.x,
   // ... (same XCD, same XCD-local order as a one-tile-per-block grid); the G128 grid is one tile each
   const int ntiles = a.nblk_m * a.nblk_n;
-  int tile = blockIdx.x;
+  int tile = BATCH ? batch_tile : (int)blockIdx.x;
   if (tile >= ntiles) return;  // (a grid / argument mismatch ends here instead of in a wild tile walk)
   int m0, n0;
   auto tile_origin = [&](int t, int& mo, int& no) {
     int bm_, bn_;
-    tile_of_block(t, a.nblk_m, a.nblk_n, a.gn, bm_, bn_);
+    if constexpr (BATCH) tile_grouped(t, a.nblk_m, a.nblk_n, a.gn, bm_, bn_);  // (the XCD split is above)
+    else tile_of_block(t, a.nblk_m, a.nblk_n, a.gn, bm_, bn_);
     mo = bm_ * BM;
     no = bn_ * BN;
   };
@@ -808,8 +836,33 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                 }
               }
             };
-            for (int p = 2 * wave; p < ntot; p += 2 * NW)
-              rescore2(epi.list[p], p + 1 < ntot ? epi.list[p + 1] : 0u, p + 1 < ntot);
+            // batches: one pair per wave at a time (64 registers of rows in flight, not 128), so that the kernel's
+            // register count leaves room on each SIMD for a wave of the other stream's prep
+            constexpr bool FIX1 = BATCH && CMVE_BATCH_FIX1;
+            if constexpr (FIX1) {
+              for (int p = wave; p < ntot; p += NW) {
+                const uint32_t e = epi.list[p];
+                const int64_t r1 = m0 + (e & 0xff), c1 = n0 + ((e >> 8) & 0xff);
+                const double inva = a.q_inv[r1], invb = a.g_inv[c1];
+                double s1;
+                if (a.q_f64) {
+                  const double* x = (const double*)a.q_raw + r1 * a.q_ld;
+                  s1 = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + c1 * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + c1 * a.g_ld, inva, invb, a.d, lane);
+                } else {
+                  const float* x = (const float*)a.q_raw + r1 * a.q_ld;
+                  s1 = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + c1 * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + c1 * a.g_ld, inva, invb, a.d, lane);
+                }
+                if (lane == 0) {
+                  if ((e >> 16) & 1u) { if (s1 > epi.sgt[r1 - m0]) lds_add_u32_async(&lds_rc[r1 - m0], 1); }
+                  if ((e >> 17) & 1u) { if (s1 > epi.sgt[BM + c1 - n0]) lds_add_u32_async(&lds_cc[c1 - n0], 1); }
+                }
+              }
+            } else {
+              for (int p = 2 * wave; p < ntot; p += 2 * NW)
+                rescore2(epi.list[p], p + 1 < ntot ? epi.list[p + 1] : 0u, p + 1 < ntot);
+            }
           } else {
             // more than the list holds (a pathological tile): each wave re-scores its own pairs in turn
 #pragma unroll
@@ -1280,7 +1333,7 @@ static void geo_fill(SimArgs& a, int64_t nq_pad, int64_t ng_pad, int bm, int bn)
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = ring_stages<MODE, G::BM, G::BN, PHASED>() *
+  const size_t lds = ring_stages<MODE, G::BM, G::BN, PHASED, G::NW>() *
                      stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
   // once per instantiation; function-local static init is thread-safe (one host thread per shard / GPU)
   static const hipError_t attr_err = hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
@@ -1963,24 +2016,46 @@ struct cmve_eval_batch {
   int qf = 0, gf = 0, mode = 0;
   bool paired = false;
   int64_t nq_pad = 0, ng_pad = 0;
+  int bm = 64, bn = 64;           // the rank tile (batch_geo_bm / _bn)
   cmve::EvalSide sq0, sg0;        // the shapes (the launch grids)
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
 };
 
-template <int MODE>
-static int launch_rank_batch(const SimArgs& a0, const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
+// the batch's rank geometry: 128 x 64 tiles (4 waves of 32 x 64, a 3-stage ring) -- a batch has tiles enough
+// to fill the chip with half as many, and each tile's fixed costs (thresholds, the re-score round trip, the
+// flush) and its L2 -> LDS bytes per MFMA shrink with it -- or the single evaluation's 64 x 64
+// (CMVE_BATCH_GEO=64: kernel studies)
+static int batch_geo_force() {
+  static const int force = [] {
+    const char* e = getenv("CMVE_BATCH_GEO");
+    return e ? atoi(e) : 0;
+  }();
+  return force;
+}
+static int batch_geo_bm(int64_t nq_pad) { return (batch_geo_force() != 64 && nq_pad % 128 == 0) ? 128 : 64; }
+static int batch_geo_bn(int64_t ng_pad) { return (batch_geo_force() == 128128 && ng_pad % 128 == 0) ? 128 : 64; }
+
+template <int MODE, int WN, int TM>
+static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
                              hipStream_t stream) {
-  using G = Geo<4, 1, 1>;
-  const size_t lds = ring_stages<MODE, G::BM, G::BN, false>() * stage_bytes<MODE, G::BM, G::BN, false>();
+  using G = Geo<4, WN, TM>;
+  const size_t lds = ring_stages<MODE, G::BM, G::BN, false, G::NW>() * stage_bytes<MODE, G::BM, G::BN, false>();
   static const hipError_t attr_err = hipFuncSetAttribute(
-      (const void*)sim_kernel<MODE, EPI_RANK, 4, 1, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (const void*)sim_kernel<MODE, EPI_RANK, 4, WN, TM, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)lds);
   CMVE_HIP(attr_err);
   const unsigned nblocks = (unsigned)((nq_pad / G::BM) * (ng_pad / G::BN));
-  hipLaunchKernelGGL((sim_kernel<MODE, EPI_RANK, 4, 1, 1, false, true>), dim3(nblocks, (unsigned)count),
-                     dim3(G::NT), (uint32_t)lds, stream, a0, tab);
+  cmve::launch(sim_kernel<MODE, EPI_RANK, 4, WN, TM, false, true>, dim3(nblocks, (unsigned)count), dim3(G::NT),
+               (uint32_t)lds, stream, SimArgs{}, tab);
   return check_launch("sim_kernel (batch)");
+}
+template <int MODE>
+static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
+                             int bm, int bn, hipStream_t stream) {
+  if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
+  return bm == 128 ? launch_rank_batch<MODE, 1, 2>(tab, count, nq_pad, ng_pad, stream)
+                   : launch_rank_batch<MODE, 1, 1>(tab, count, nq_pad, ng_pad, stream);
 }
 
 extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* const* g,
@@ -2001,7 +2076,12 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
     if (st) return st;
     CMVE_REQUIRE(P.inline_fix, "cmve_eval_batch_create: batches take the G64 geometry (fewer than 128 tiles of "
                                "128^2, e.g. 1,000 x 1,000) with the inline fix-up");
-    CMVE_REQUIRE(P.c.stamps == nullptr, "cmve_eval_batch_create: CMVE_EVAL_DBG stamps are per evaluation");
+    if (P.c.stamps) {  // kernel studies (CMVE_EVAL_DBG & 128): the first evaluation's prep / finish blocks, and
+                       // every evaluation's rank tiles while the stamp buffer's 1,024 tile slots last
+      const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad)) * (g[i]->n_pad / batch_geo_bn(g[i]->n_pad));
+      P.a.dbg_stamps = (i + 1) * per <= 1024 ? P.c.stamps + 3 * 1024 * 8 + (size_t)i * per * 8 : nullptr;
+      if (i > 0) P.c.stamps = nullptr;
+    }
     if (i == 0) {
       P0 = P;
     } else {
@@ -2014,7 +2094,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
                      "cmve_eval_batch_create: evaluations %d and %d share a workspace or an output", j, i);
     }
     items[(size_t)i] = cmve::EvalItem{P.sq, P.sg, P.c};
-    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, 64, 64);  // (launch_geo fills these for a single launch)
+    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad), batch_geo_bn(g[i]->n_pad));  // (launch_geo's, for one launch)
     args[(size_t)i] = P.a;
   }
   auto* b = new cmve_eval_batch;
@@ -2025,6 +2105,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->paired = P0.paired;
   b->nq_pad = q[0]->n_pad;
   b->ng_pad = g[0]->n_pad;
+  b->bm = batch_geo_bm(b->nq_pad);
+  b->bn = batch_geo_bn(b->ng_pad);
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
@@ -2042,19 +2124,44 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   return CMVE_OK;
 }
 
-extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b) {
+// timing_slot >= 0: the three launches' own start / stop into that slot of h's ring (cmve_eval_kernel_timing:
+// prep, rank GEMM, 0, finish -- durations of the whole batch's launches) and the event spans (cmve_eval_timing)
+extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_slot) {
   CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
+  hipEvent_t* ev = nullptr;
+  hipEvent_t* kev = nullptr;
+  if (timing_slot >= 0) {
+    ev = h->eval_ev[timing_slot];
+    for (int k = 0; k < 4; ++k)
+      if (!ev[k]) CMVE_HIP(hipEventCreate(&ev[k]));
+    kev = h->eval_kev[timing_slot];
+    for (int k = 0; k < 8; ++k)
+      if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
+    h->eval_no_fix[timing_slot] = true;
+  }
+  auto arm = [&](int k) {
+    if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
+  };
   hipStream_t s = h->stream;
+  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
+  arm(0);
   int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
   if (st) return st;
-  SimArgs a0{};  // (the by-value argument is unused by the batched kernel)
+  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
+  arm(1);
   switch (b->mode) {
-    case CMVE_SIM_F16: st = launch_rank_batch<CMVE_SIM_F16>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
-    case CMVE_SIM_BF16: st = launch_rank_batch<CMVE_SIM_BF16>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
-    default: st = launch_rank_batch<CMVE_SIM_BF16X3>(a0, b->d_args, b->count, b->nq_pad, b->ng_pad, s); break;
+    case CMVE_SIM_F16: st = launch_rank_batch<CMVE_SIM_F16>(b->d_args, b->count, b->nq_pad, b->ng_pad, b->bm, b->bn, s); break;
+    case CMVE_SIM_BF16: st = launch_rank_batch<CMVE_SIM_BF16>(b->d_args, b->count, b->nq_pad, b->ng_pad, b->bm, b->bn, s); break;
+    default: st = launch_rank_batch<CMVE_SIM_BF16X3>(b->d_args, b->count, b->nq_pad, b->ng_pad, b->bm, b->bn, s); break;
   }
   if (st) return st;
-  return cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, 2, s);
+  if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
+  arm(3);
+  st = cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, 2, s);
+  if (st) return st;
+  if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
+  return CMVE_OK;
 }
 
 extern "C" int cmve_eval_batch_destroy(cmve_eval_batch_t b) {

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 16
+#define CMVE_ABI_VERSION 17
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -425,14 +425,18 @@ int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
  * leave most of the chip idle, a batch fills it.  The argument blocks are built and copied to the device at
  * create time (every pointer is baked in: refill the raw rows in place between runs, as for the graph form);
  * run enqueues the three launches on h's stream; the results equal cmve_eval_ranks' bit for bit.  Batches take
- * the G64 geometry (fewer than 128 tiles of 128^2) with the rank GEMM's inline fp64 re-score (no overflow).
+ * the small-problem geometry (fewer than 128 tiles of 128^2, e.g. 1,000 x 1,000) with the rank GEMM's inline fp64
+ * re-score (no overflow); the batch's rank GEMM runs 128 x 64 tiles, each XCD taking a contiguous run of the
+ * (evaluation, tile) pairs.
  * create synchronises (it uploads the table). */
 typedef struct cmve_eval_batch* cmve_eval_batch_t;
 int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* const* g, int32_t mode,
                            const int64_t* row_off, const int32_t* row_idx, const int64_t* col_off,
                            const int32_t* col_idx, void* const* ws, int64_t ws_bytes, int64_t cand_cap,
                            int64_t* const* out, cmve_eval_batch_t* batch);
-int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch);
+/* timing_slot: -1, or a slot of h's timing ring receiving the batch's launch durations (cmve_eval_kernel_timing:
+ * prep, rank GEMM, 0, finish; cmve_eval_timing: the event spans), as for cmve_eval_ranks */
+int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch, int32_t timing_slot);
 int cmve_eval_batch_destroy(cmve_eval_batch_t batch);
 typedef struct cmve_eval_graph* cmve_eval_graph_t;
 int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,

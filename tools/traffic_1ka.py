@@ -26,11 +26,13 @@ ROLES = ("pack_gt_scores", "rank_gemm", "fixup", "ranks_recall")
 
 
 def role(name):
-    if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name:
+    # (single evaluations and batches: eval_*_batch_kernel, sim_kernel<..., true>; one profile holds one form)
+    if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name or "eval_prep_pair_batch_kernel" in name \
+            or "eval_prep_batch_kernel" in name:
         return "pack_gt_scores"
     if "eval_fix_kernel" in name:
         return "fixup"
-    if "eval_finish_kernel" in name:
+    if "eval_finish_kernel" in name or "eval_finish_batch_kernel" in name:
         return "ranks_recall"
     if "sim_kernel<2, 1" in name:
         return "rank_gemm"
@@ -49,15 +51,17 @@ def main(outdir, tag):
             k = role(r.get("Kernel_Name", ""))
             if k and r.get("Counter_Name") == counter:
                 per[k][counter].append(float(r["Counter_Value"]))
-    dur = defaultdict(list)
+    dur, evals = defaultdict(list), defaultdict(list)
     for r in rows(os.path.join(outdir, "trace", "**", "*kernel_trace.csv")):
         k = role(r.get("Kernel_Name", ""))
         if k:
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+            evals[k].append(int(r.get("Grid_Size_Y") or 1))  # batches: grid y = the evaluations
     kernels = {}
     for k in ROLES:
         f, w = per[k]["FETCH_SIZE"], per[k]["WRITE_SIZE"]
         e = {"launches_traced": len(dur[k]),
+             "evaluations_per_launch": (max(set(evals[k]), key=evals[k].count)) if evals[k] else None,
              "trace_avg_ms": (sum(dur[k]) / len(dur[k])) if dur[k] else None,
              "trace_total_ms": sum(dur[k]),
              "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
