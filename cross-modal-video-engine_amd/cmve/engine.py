@@ -637,13 +637,19 @@ class RankBatch:
         self.sessions, self.outs, self.stream = sessions, outs, stream
         self._h = stream_handle(s0.device, stream) if stream is not None else None
 
-    def run(self, timing_slot: int = -1):
+    def run(self, timing_slot: int = -1, wait_current: bool = True):
         """Enqueue the batch; ``timing_slot`` >= 0 records its launches' durations in that slot of the stream
-        handle's timing ring (``kernel_timing``)."""
+        handle's timing ring (``kernel_timing``).  With a batch stream the run first waits for the work already
+        enqueued on the caller's current stream (the producer that refilled the inputs, as RankSession.enqueue
+        does); ``wait_current=False`` skips that for inputs known to be complete."""
         if not self._b:
             raise RuntimeError("RankBatch.run: the batch was closed")
         if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
             raise RuntimeError("RankBatch.run: a session's workspace was regrown after the batch was built")
+        if self.stream is not None and wait_current:
+            cur = torch.cuda.current_stream(self.sessions[0].device)
+            if cur.cuda_stream != self.stream.cuda_stream:
+                self.stream.wait_stream(cur)
         h = self._h if self._h is not None else handle(self.sessions[0].device)
         check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
 

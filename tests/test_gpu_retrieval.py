@@ -790,3 +790,46 @@ def test_rank_batch_equals_sessions(golden, torch_cuda, case):
     torch.cuda.synchronize()
     assert torch.equal(sess[1].out, ref[2])
     b.close()
+
+
+@pytest.mark.gpu
+def test_rank_batch_stream_outs_timing(golden, torch_cuda):
+    """A batch of one and a batch of three on their own stream with caller outputs: a refill enqueued on the
+    default stream just before run() is seen without a host synchronisation (run orders its stream after the
+    caller's), the outputs land in the caller's rows, and a timing slot records the three launches."""
+    import torch
+    from cmve import engine
+    v, c, vid, cid = _c1()
+    v2t_gt, t2v_gt = R.get_gt(vid, cid)
+    rows, cols = [t2v_gt[i] for i in range(len(cid))], v2t_gt
+    g = golden("retrieval_c1")
+    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
+    good = (torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    st = torch.cuda.Stream()
+    for k in (1, 3):
+        sets = [(torch.zeros_like(good[0]), torch.zeros_like(good[1])) for _ in range(k)]
+        for cq, gv in sets:
+            cq.copy_(good[0])
+            gv.copy_(good[1])
+        sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64) for _ in range(k)]
+        for s_, (cq, gv) in zip(sess, sets):
+            s_.run(cq, gv)  # sizes the lists
+        outs = torch.full((k, sess[0].out.numel()), -7, dtype=torch.int64, device="cuda")
+        b = engine.RankBatch(sess, sets, outs=list(outs), stream=st)
+        # scramble, then refill on the default stream and run at once: the batch must see the refill
+        for cq, gv in sets:
+            cq.zero_()
+            gv.zero_()
+        torch.cuda.synchronize()
+        for cq, gv in sets:
+            cq.copy_(good[0])
+            gv.copy_(good[1])
+        b.run(timing_slot=0)
+        st.synchronize()
+        h = outs.cpu().numpy()
+        for i in range(k):
+            assert h[i, 9] == 0
+            assert np.array_equal(h[i, 16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[i, 16 + n_q:], g["v2t_ranks"])
+        ms = b.kernel_timing(0)
+        assert ms[0] > 0 and ms[1] > 0 and ms[2] == 0 and ms[3] > 0
+        b.close()
