@@ -2038,7 +2038,10 @@ static int batch_geo_force() {
   return force;
 }
 static int batch_geo_bm(int64_t nq_pad) { return (batch_geo_force() != 64 && nq_pad % 128 == 0) ? 128 : 64; }
-static int batch_geo_bn(int64_t ng_pad) { return (batch_geo_force() == 128128 && ng_pad % 128 == 0) ? 128 : 64; }
+// (128 x 128: split-bf16's 3 stages of both planes would not fit the LDS)
+static int batch_geo_bn(int64_t ng_pad, int mode) {
+  return (batch_geo_force() == 128128 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3) ? 128 : 64;
+}
 
 template <int MODE, int WN, int TM>
 static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
@@ -2057,7 +2060,8 @@ static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int6
 template <int MODE>
 static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
                              int bm, int bn, hipStream_t stream) {
-  if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
+  if constexpr (MODE != CMVE_SIM_BF16X3)
+    if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
   return bm == 128 ? launch_rank_batch<MODE, 1, 2>(tab, count, nq_pad, ng_pad, stream)
                    : launch_rank_batch<MODE, 1, 1>(tab, count, nq_pad, ng_pad, stream);
 }
@@ -2082,7 +2086,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
                                "128^2, e.g. 1,000 x 1,000) with the inline fix-up");
     if (P.c.stamps) {  // kernel studies (CMVE_EVAL_DBG & 128): the first evaluation's prep / finish blocks, and
                        // every evaluation's rank tiles while the stamp buffer's 1,024 tile slots last
-      const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad)) * (g[i]->n_pad / batch_geo_bn(g[i]->n_pad));
+      const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad)) *
+                          (g[i]->n_pad / batch_geo_bn(g[i]->n_pad, mode_flags & 0xff));
       P.a.dbg_stamps = (i + 1) * per <= 1024 ? P.c.stamps + 3 * 1024 * 8 + (size_t)i * per * 8 : nullptr;
       if (i > 0) P.c.stamps = nullptr;
     }
@@ -2098,7 +2103,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
                      "cmve_eval_batch_create: evaluations %d and %d share a workspace or an output", j, i);
     }
     items[(size_t)i] = cmve::EvalItem{P.sq, P.sg, P.c};
-    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad), batch_geo_bn(g[i]->n_pad));  // (launch_geo's, for one launch)
+    // (launch_geo fills these for a single launch)
+    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad), batch_geo_bn(g[i]->n_pad, mode_flags & 0xff));
     args[(size_t)i] = P.a;
   }
   auto* b = new cmve_eval_batch;
@@ -2110,7 +2116,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->nq_pad = q[0]->n_pad;
   b->ng_pad = g[0]->n_pad;
   b->bm = batch_geo_bm(b->nq_pad);
-  b->bn = batch_geo_bn(b->ng_pad);
+  b->bn = batch_geo_bn(b->ng_pad, b->mode);
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
