@@ -738,7 +738,7 @@ def test_paired_prep_equals_general_prep(torch_cuda, dt):
     assert r1[3] == n
 
 
-@pytest.mark.parametrize("case", ["c1_paired_f64", "multi_gt_f32"])
+@pytest.mark.parametrize("case", ["c1_paired_f64", "multi_gt_f32", "multi_gt_f32_bf16", "multi_gt_f32_bf16x3"])
 def test_rank_batch_equals_sessions(golden, torch_cuda, case):
     """RankBatch (cmve_eval_batch_*: one prep, one rank GEMM, one finish launch over several evaluations)
     against each session's own evaluation of the same inputs: every output word (R@K head, pair total, ranks)
@@ -768,12 +768,14 @@ def test_rank_batch_equals_sessions(golden, torch_cuda, case):
             qs = (gal[[l[0] for l in rows]] + 0.9 * rng.standard_normal((nq, d))).astype(np.float32)
             sets.append((torch.from_numpy(qs).cuda(), torch.from_numpy(gal).cuda()))
     n_q, n_g, d = sets[0][0].shape[0], sets[0][1].shape[0], sets[0][0].shape[1]
+    from cmve import _lib
+    mode = {"multi_gt_f32_bf16": _lib.SIM_BF16, "multi_gt_f32_bf16x3": _lib.SIM_BF16X3}.get(case, _lib.SIM_F16)
     ref = []
     for cq, gv in sets:
-        s = engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt)
+        s = engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt, mode=mode)
         s.run(cq, gv)
         ref.append(s.out.clone())
-    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt) for _ in sets]
+    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=dt, mode=mode) for _ in sets]
     b = engine.RankBatch(sess, sets)
     for _ in range(2):
         b.run()
