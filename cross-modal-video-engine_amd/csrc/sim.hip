@@ -325,7 +325,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
     batch_item = L / per;
     batch_tile = L - batch_item * per;
   }
-  const SimArgs a = BATCH ? tab[batch_item] : a_arg;
+  const SimArgs& a = BATCH ? tab[batch_item] : a_arg;
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
