@@ -235,8 +235,8 @@ constexpr size_t stage_bytes() {
 // (8 per wave per K-tile, ~2.7 us for the first 7 K-tiles of an 8-deep ring in the stamps), so a deeper
 // ring gains nothing alone, while 64 KiB lets two evaluations' rank GEMMs share a CU (two HIP streams:
 // 31.0 -> 26.6 us per evaluation, tools/eval_pipe.py)
-// The 128 x 64 ring (K14 batches only, cmve_eval_batch_*): 3 stages of 24 KiB, so that two blocks still share a CU
-// (2 x (72 KiB + the epilogue scratch) <= 160 KiB)
+// The K14 batches' rings (cmve_eval_batch_*): 128 x 128 with 8 waves, 3 stages of 32 KiB (96 KiB + the epilogue
+// scratch: room beside it for another stream's prep blocks), and 128 x 64 (split-bf16), 3 stages of 24 KiB
 template <int MODE, int BM, int BN, bool PHASED, int NW = 4>
 constexpr int ring_stages() {
 #ifndef CMVE_G64_STAGES
@@ -2026,10 +2026,12 @@ struct cmve_eval_batch {
   SimArgs* d_args = nullptr;
 };
 
-// the batch's rank geometry: 128 x 64 tiles (4 waves of 32 x 64, a 3-stage ring) -- a batch has tiles enough
-// to fill the chip with half as many, and each tile's fixed costs (thresholds, the re-score round trip, the
-// flush) and its L2 -> LDS bytes per MFMA shrink with it -- or the single evaluation's 64 x 64
-// (CMVE_BATCH_GEO=64: kernel studies)
+// the batch's rank geometry: 128 x 128 tiles (8 waves of 32 x 64, a 3-stage ring of 32 KiB stages, one block of
+// 105 KiB per CU) -- a batch has tiles enough to fill the chip with a quarter as many as 64 x 64, and each tile's
+// fixed costs (thresholds, the re-score round trip, the flush) and its L2 -> LDS bytes per MFMA shrink with it;
+// the 55 KiB of LDS and the registers it leaves let another stream's prep blocks share the CU (128 x 64, two
+// 4-wave blocks per CU, filled the LDS: 9.7e10 vs 1.12e11 pairs/s at three streams).  Split-bf16 (whose ring
+// holds both planes) takes 128 x 64; CMVE_BATCH_GEO = 64 / 12864 force 64 x 64 / 128 x 64 (kernel studies).
 static int batch_geo_force() {
   static const int force = [] {
     const char* e = getenv("CMVE_BATCH_GEO");
@@ -2038,9 +2040,9 @@ static int batch_geo_force() {
   return force;
 }
 static int batch_geo_bm(int64_t nq_pad) { return (batch_geo_force() != 64 && nq_pad % 128 == 0) ? 128 : 64; }
-// (128 x 128: split-bf16's 3 stages of both planes would not fit the LDS)
-static int batch_geo_bn(int64_t ng_pad, int mode) {
-  return (batch_geo_force() == 128128 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3) ? 128 : 64;
+static int batch_geo_bn(int64_t nq_pad, int64_t ng_pad, int mode) {
+  const int f = batch_geo_force();
+  return (f != 64 && f != 12864 && nq_pad % 128 == 0 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3) ? 128 : 64;
 }
 
 template <int MODE, int WN, int TM>
@@ -2087,7 +2089,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
     if (P.c.stamps) {  // kernel studies (CMVE_EVAL_DBG & 128): the first evaluation's prep / finish blocks, and
                        // every evaluation's rank tiles while the stamp buffer's 1,024 tile slots last
       const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad)) *
-                          (g[i]->n_pad / batch_geo_bn(g[i]->n_pad, mode_flags & 0xff));
+                          (g[i]->n_pad / batch_geo_bn(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff));
       P.a.dbg_stamps = (i + 1) * per <= 1024 ? P.c.stamps + 3 * 1024 * 8 + (size_t)i * per * 8 : nullptr;
       if (i > 0) P.c.stamps = nullptr;
     }
@@ -2104,7 +2106,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
     }
     items[(size_t)i] = cmve::EvalItem{P.sq, P.sg, P.c};
     // (launch_geo fills these for a single launch)
-    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad), batch_geo_bn(g[i]->n_pad, mode_flags & 0xff));
+    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad),
+             batch_geo_bn(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff));
     args[(size_t)i] = P.a;
   }
   auto* b = new cmve_eval_batch;
@@ -2116,7 +2119,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->nq_pad = q[0]->n_pad;
   b->ng_pad = g[0]->n_pad;
   b->bm = batch_geo_bm(b->nq_pad);
-  b->bn = batch_geo_bn(b->ng_pad, b->mode);
+  b->bn = batch_geo_bn(b->nq_pad, b->ng_pad, b->mode);
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
