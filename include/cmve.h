@@ -426,8 +426,8 @@ int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
  * create time (every pointer is baked in: refill the raw rows in place between runs, as for the graph form);
  * run enqueues the three launches on h's stream; the results equal cmve_eval_ranks' bit for bit.  Batches take
  * the small-problem geometry (fewer than 128 tiles of 128^2, e.g. 1,000 x 1,000) with the rank GEMM's inline fp64
- * re-score (no overflow); the batch's rank GEMM runs 128 x 64 tiles, each XCD taking a contiguous run of the
- * (evaluation, tile) pairs.
+ * re-score (no overflow); the batch's rank GEMM runs 128 x 128 tiles (split-bf16: 128 x 64), each XCD taking a
+ * contiguous run of the (evaluation, tile) pairs.
  * create synchronises (it uploads the table). */
 typedef struct cmve_eval_batch* cmve_eval_batch_t;
 int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* const* g, int32_t mode,
