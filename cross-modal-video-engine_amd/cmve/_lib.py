@@ -29,6 +29,7 @@ EVAL_TIMING_SLOTS = 32
 EVAL_OUT_HEAD = 16
 EVAL_PAIRED = 0x100  # CMVE_EVAL_PAIRED
 DIST_UNIQUE_ID_BYTES = 128  # CMVE_DIST_UNIQUE_ID_BYTES
+DIST_SUM, DIST_MAX = 0, 1  # CMVE_DIST_SUM / CMVE_DIST_MAX
 PACK_RAW = 1
 POOL_MEAN_VALID, POOL_MEAN_ALL, POOL_MAX_MASKED_ZERO, POOL_MAX_ALL = 0, 1, 2, 3
 PW_SQ_L2, PW_L2, PW_L1, PW_ORDER, PW_JACCARD, PW_DOT = 0, 1, 2, 3, 4, 5
@@ -117,6 +118,9 @@ SIGNATURES = {
     "cmve_dist_allgather_q": (C.c_int, [_vp, _vp, _i64, _i64, _vp]),
     "cmve_dist_reduce_rank": (C.c_int, [_vp, _vp, _vp, _i64]),
     "cmve_dist_allgather_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "cmve_dist_allreduce": (C.c_int, [_vp, _vp, _i64, _i32, _i32]),
+    "cmve_dist_allgather": (C.c_int, [_vp, _vp, _i64, _i32, _vp]),
+    "cmve_dist_size": (C.c_int, [_vp, _vp, _vp]),
     "cmve_dist_destroy": (C.c_int, [_vp]),
     "cmve_merge_topk": (C.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _vp]),
     "cmve_rank_from_matrix": (C.c_int, [_vp, _vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _vp]),
@@ -156,7 +160,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

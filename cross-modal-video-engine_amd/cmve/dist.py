@@ -86,6 +86,90 @@ class TorchComm:
             dist.barrier()
 
 
+class CAbiComm:
+    """The torch.distributed ranks over the C ABI's own RCCL communicator (``cmve_dist_*``, csrc/dist.hip): the
+    collectives a host without torch would call, driven through the same ShardedGallery coordination.  The
+    128-byte unique id is made on rank 0 and broadcast over the process group (``uid`` given: used as is,
+    e.g. by a host with its own bootstrap); every collective is enqueued on the caller's current stream.
+    At world 1 the collectives still run (identity gathers / reductions), so the path is exercised on one GPU."""
+
+    always = True  # run the collectives at world 1 too (see _solo)
+    _TYPES = {torch.float32: _lib.CMVE_F32, torch.float64: _lib.CMVE_F64, torch.int32: _lib.CMVE_I32,
+              torch.int64: _lib.CMVE_I64}
+
+    def __init__(self, device: Optional[torch.device] = None, rank: Optional[int] = None,
+                 world: Optional[int] = None, uid: Optional[bytes] = None):
+        import ctypes as C
+        r0, w0 = _world()
+        self.rank = r0 if rank is None else int(rank)
+        self.world = w0 if world is None else int(world)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        if uid is None:
+            buf = C.create_string_buffer(_lib.DIST_UNIQUE_ID_BYTES)
+            if self.rank == 0:
+                _lib.check(_lib.lib.cmve_dist_unique_id(buf), "cmve_dist_unique_id")
+            if self.world > 1:
+                obj = [bytes(buf.raw) if self.rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                buf = C.create_string_buffer(obj[0], _lib.DIST_UNIQUE_ID_BYTES)
+        else:
+            buf = C.create_string_buffer(bytes(uid), _lib.DIST_UNIQUE_ID_BYTES)
+        h = C.c_void_p()
+        _lib.check(_lib.lib.cmve_create(idx, C.c_void_p(torch.cuda.current_stream(idx).cuda_stream), C.byref(h)),
+                   "cmve_create")
+        self._h = h.value
+        _lib.check(_lib.lib.cmve_dist_init(self._h, self.world, self.rank, buf), "cmve_dist_init")
+        n, rk = C.c_int32(), C.c_int32()
+        _lib.check(_lib.lib.cmve_dist_size(self._h, C.byref(n), C.byref(rk)), "cmve_dist_size")
+        if (n.value, rk.value) != (self.world, self.rank):
+            raise RuntimeError(f"CAbiComm: communicator is rank {rk.value} of {n.value}, expected "
+                               f"{self.rank} of {self.world}")
+
+    def _code(self, t: torch.Tensor) -> int:
+        if t.dtype not in self._TYPES or not t.is_contiguous() or t.device != self.device:
+            raise ValueError(f"CAbiComm: contiguous {list(self._TYPES)} tensors on {self.device} only, got "
+                             f"{t.dtype} on {t.device}")
+        return self._TYPES[t.dtype]
+
+    def _on_current(self):
+        import ctypes as C
+        _lib.check(_lib.lib.cmve_set_stream(self._h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "cmve_set_stream")
+
+    def all_reduce(self, t: torch.Tensor, op: str) -> torch.Tensor:
+        """In place; op 'sum' or 'max'."""
+        code = self._code(t)
+        self._on_current()
+        _lib.check(_lib.lib.cmve_dist_allreduce(self._h, engine._ptr(t), t.numel(), code,
+                                                _lib.DIST_SUM if op == "sum" else _lib.DIST_MAX),
+                   "cmve_dist_allreduce")
+        return t
+
+    def all_gather_into(self, out: torch.Tensor, x: torch.Tensor, async_op: bool = False):
+        """out = cat over ranks of x (equal shapes), enqueued on the current stream (async_op: a completed
+        Work -- the stream order already holds every later reader)."""
+        x = x.contiguous()
+        code = self._code(x)
+        if out.dtype != x.dtype or out.numel() != self.world * x.numel() or not out.is_contiguous():
+            raise ValueError("CAbiComm.all_gather_into: out must be world x the input, same dtype, contiguous")
+        self._on_current()
+        _lib.check(_lib.lib.cmve_dist_allgather(self._h, engine._ptr(x), x.numel(), code, engine._ptr(out)),
+                   "cmve_dist_allgather")
+        return _Done() if async_op else None
+
+    def barrier(self):
+        t = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.all_reduce(t, "sum")
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def close(self):
+        if self._h:
+            _lib.lib.cmve_dist_destroy(self._h)
+            _lib.lib.cmve_destroy(self._h)
+            self._h = None
+
+
 class ThreadComm:
     """One shard's view of a ``LocalGroup``: the collectives of TorchComm between threads of one
     process.  Every exchange completes its inputs on the caller's stream first and its outputs
@@ -177,6 +261,11 @@ class LocalGroup:
         return results
 
 
+def _solo(comm) -> bool:
+    """A world-1 communicator whose collectives may be skipped (CAbiComm runs them even then: `always`)."""
+    return comm.world == 1 and not getattr(comm, "always", False)
+
+
 def _comm(comm):
     """A communicator from None (TorchComm), an int world size (legacy: TorchComm, which must agree),
     or a communicator object."""
@@ -216,7 +305,7 @@ def decode_gt_scores(key: torch.Tensor) -> torch.Tensor:
 def merge_gt_scores(sgt_partial: torch.Tensor, comm=None) -> torch.Tensor:
     """all-reduce(MAX) of per-shard best-GT scores (encode / MAX / decode)."""
     comm = _comm(comm)
-    if comm.world == 1:
+    if _solo(comm):
         return sgt_partial
     s = encode_gt_scores(sgt_partial)
     comm.all_reduce(s, "max")
@@ -232,7 +321,7 @@ def gather_rows_async(x_local: torch.Tensor, out: torch.Tensor, comm=None):
     """all_gather_into_tensor(out, x_local) as an async collective (RCCL runs it on its own stream):
     returns the Work to .wait() on before reading `out`, or None at world 1 (plain copy)."""
     comm = _comm(comm)
-    if comm.world == 1:
+    if _solo(comm):
         out.copy_(x_local)
         return None
     return comm.all_gather_into(out, x_local.contiguous(), async_op=True)
@@ -241,7 +330,7 @@ def gather_rows_async(x_local: torch.Tensor, out: torch.Tensor, comm=None):
 def all_gather_rows(x_local: torch.Tensor, comm=None) -> torch.Tensor:
     """Rows of every rank in rank order (equal row counts on every rank)."""
     comm = _comm(comm)
-    if comm.world == 1:
+    if _solo(comm):
         return x_local
     out = torch.empty((comm.world * x_local.shape[0],) + tuple(x_local.shape[1:]), dtype=x_local.dtype,
                       device=x_local.device)
@@ -253,7 +342,7 @@ def all_gather_var(x_local: torch.Tensor, comm=None) -> torch.Tensor:
     """Rows of every rank in rank order when ranks hold different row counts: the counts are
     gathered first, every rank pads to the largest, and the padding is dropped after the gather."""
     comm = _comm(comm)
-    if comm.world == 1:
+    if _solo(comm):
         return x_local
     n = torch.tensor([x_local.shape[0]], dtype=torch.int64, device=x_local.device)
     ns = all_gather_rows(n, comm).tolist()
@@ -269,7 +358,7 @@ def all_gather_var(x_local: torch.Tensor, comm=None) -> torch.Tensor:
 def any_flag(flag: torch.Tensor, comm=None) -> torch.Tensor:
     """OR of a per-rank boolean over the ranks (all-reduce MAX), so that all ranks take the same branch."""
     comm = _comm(comm)
-    if comm.world == 1:
+    if _solo(comm):
         return flag
     o = flag.to(torch.int32).reshape(1)
     comm.all_reduce(o, "max")
@@ -299,7 +388,7 @@ def gather_topk(idx_global: torch.Tensor, scores: torch.Tensor, comm=None):
     world = comm.world
     ids = idx_global.to(torch.int64).contiguous()
     sc = scores.to(torch.float64).contiguous()
-    if world == 1:
+    if _solo(comm):
         return ids, sc
     n_q, kk = ids.shape
     gi = all_gather_rows(ids, comm)

@@ -575,6 +575,8 @@ class RankSession:
                 self.host.copy_(self.out, non_blocking=True)
                 torch.cuda.current_stream(self.device).synchronize()
             need = int(self.host[9])
+            if int(self.host[11]):  # (the paired prep's per-caption check of CMVE_EVAL_PAIRED)
+                raise _lib.CmveError("RankSession: the GT lists are not a one-to-one pairing")
             if need == 0:
                 break
             self._alloc(max(need, 2 * self.cap))  # a bucket overflowed: the counts are incomplete
@@ -607,6 +609,12 @@ class RankBatch:
             if (s.q.n, s.g.n, s.q.d, s.dtype, s.mode, s.paired) != (s0.q.n, s0.g.n, s0.q.d, s0.dtype, s0.mode,
                                                                    s0.paired) or not same_lists:
                 raise ValueError("RankBatch: sessions must share sizes, dtype, mode and GT lists")
+        # one undecided-pair capacity for the whole batch (the C table holds one cand_cap and workspace size): a
+        # session whose list was grown sets it, the others are grown to it here, before any input is bound
+        cap = max(s.cap for s in sessions)
+        for s in sessions:
+            if s.cap != cap:
+                s._alloc(cap)
         outs = [s.out for s in sessions] if outs is None else list(outs)
         for s, o in zip(sessions, outs):
             if o.dtype != torch.int64 or not o.is_contiguous() or o.numel() < s.out.numel():
@@ -623,8 +631,9 @@ class RankBatch:
         self._g = (C.POINTER(Rows) * n)(*[C.pointer(s.g.desc) for s in sessions])
         self._ws = (C.c_void_p * n)(*[s.ws.data_ptr() for s in sessions])
         self._out = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
-        ws_bytes = min(s.ws.numel() for s in sessions)
-        cap = min(s.cap for s in sessions)
+        ws_bytes = sessions[0].ws.numel()
+        if any(s.cap != cap or s.ws.numel() != ws_bytes for s in sessions):
+            raise ValueError("RankBatch: sessions must share one undecided-pair capacity and workspace size")
         r = s0.row if s0.row is not None else (None, None)
         c = s0.col if s0.col is not None else (None, None)
         mode = s0.mode | (_lib.EVAL_PAIRED if s0.paired else 0)

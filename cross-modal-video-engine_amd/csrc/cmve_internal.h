@@ -270,8 +270,31 @@ __device__ __forceinline__ double row_inv_norm(double ss, double eps, int flags)
 // so the f16 conversion need not be correctly rounded from fp64: it goes through fp32, which the
 // hardware converts directly -- gfx950 has no fp64 -> fp16 instruction)
 struct PackAcc {
-  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
+  double e1 = 0.0, e2 = 0.0, e3 = 0.0, e4 = 0.0;  // e4: the r8 residual plane's squared residuals
 };
+
+// ---- the 8-bit residual plane of the fp16 rank operand (K14 level-2 re-score) ----
+// An element x (fp64, normalised) packed to fp16 h leaves r3 = x - h, |r3| <= ulp(h) / 2.  r8 stores r3 in units
+// of ulp(h) / 256 (ulp(h) = 2^(max(E, 1) - 25) for h's biased exponent field E: subnormals share E = 1's
+// spacing), rounded and clamped to [-127, 127]:  x2 = h + r8 * 2^(max(E, 1) - 33).  x2 is EXACT in fp32 (h has
+// 11 significant bits with its last at 2^(E'-25), the residual term 8 more below them), so a product of two
+// such values is exact in fp64.  err4 = x - x2 (computed in fp64; the bound's slack covers its rounding).
+__device__ __forceinline__ int r8_shift(uint16_t hbits) {
+  const int e = (hbits >> 10) & 31;
+  return 33 - (e > 1 ? e : 1);
+}
+__device__ __forceinline__ int8_t r8_elem(double r3, uint16_t hbits, double& err4) {
+  const int sh = r8_shift(hbits);
+  double t = rint(ldexp(r3, sh));
+  t = t == t ? fmin(127.0, fmax(-127.0, t)) : 0.0;  // (a NaN row's pairs are never in a band)
+  err4 = r3 - ldexp(t, -sh);
+  return (int8_t)(int)t;
+}
+// x2 of r8_elem as fp32 (exact)
+__device__ __forceinline__ float r8_value(uint16_t hbits, int8_t r) {
+  const float h = (float)__builtin_bit_cast(_Float16, hbits);
+  return h + ldexpf((float)r, -r8_shift(hbits));
+}
 __device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h, uint16_t& l, uint16_t& f,
                                           PackAcc& acc) {
   const float xf = (float)xh;

@@ -167,6 +167,52 @@ extern "C" int cmve_dist_allgather_topk(cmve_handle_t h, const int64_t* ids, con
                            out_ids, out_scores);
 }
 
+// the plain collectives a host needs beside the three above (the two-direction exchange's SUM carries int64
+// counts and R@K sums; the layout check and the v2t rank gather move int64 rows)
+static bool nccl_type(int32_t dt, ncclDataType_t& t) {
+  switch (dt) {
+    case CMVE_F32: t = ncclFloat32; return true;
+    case CMVE_F64: t = ncclFloat64; return true;
+    case CMVE_I32: t = ncclInt32; return true;
+    case CMVE_I64: t = ncclInt64; return true;
+    default: return false;
+  }
+}
+
+extern "C" int cmve_dist_allreduce(cmve_handle_t h, void* buf, int64_t count, int32_t dtype, int32_t op) {
+  CMVE_REQUIRE(h && h->comm, "cmve_dist_allreduce: handle has no communicator (cmve_dist_init)");
+  ncclDataType_t t;
+  CMVE_REQUIRE(nccl_type(dtype, t), "cmve_dist_allreduce: unsupported dtype %d", dtype);
+  CMVE_REQUIRE(op == CMVE_DIST_SUM || op == CMVE_DIST_MAX, "cmve_dist_allreduce: op must be SUM or MAX");
+  CMVE_REQUIRE(count >= 0 && (count == 0 || buf), "cmve_dist_allreduce: bad argument");
+  if (count == 0) return CMVE_OK;
+  const RcclApi* api = rccl_api();
+  CMVE_RCCL(api, api->all_reduce(buf, buf, (size_t)count, t, op == CMVE_DIST_SUM ? ncclSum : ncclMax,
+                                 (ncclComm_t)h->comm, h->stream),
+            "cmve_dist_allreduce");
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_allgather(cmve_handle_t h, const void* local, int64_t count, int32_t dtype, void* gathered) {
+  CMVE_REQUIRE(h && h->comm, "cmve_dist_allgather: handle has no communicator (cmve_dist_init)");
+  ncclDataType_t t;
+  CMVE_REQUIRE(nccl_type(dtype, t), "cmve_dist_allgather: unsupported dtype %d", dtype);
+  CMVE_REQUIRE(count >= 0 && (count == 0 || (local && gathered)), "cmve_dist_allgather: bad argument");
+  if (count == 0) return CMVE_OK;
+  const RcclApi* api = rccl_api();
+  CMVE_RCCL(api, api->all_gather(local, gathered, (size_t)count, t, (ncclComm_t)h->comm, h->stream),
+            "cmve_dist_allgather");
+  return CMVE_OK;
+}
+
+extern "C" int cmve_dist_size(cmve_handle_t h, int32_t* nranks, int32_t* rank) {
+  CMVE_REQUIRE(h && nranks && rank, "cmve_dist_size: NULL argument");
+  CMVE_REQUIRE(h->comm, "cmve_dist_size: handle has no communicator (cmve_dist_init)");
+  *nranks = h->nranks;
+  *rank = h->rank;
+  return CMVE_OK;
+}
+
 extern "C" int cmve_dist_destroy(cmve_handle_t h) {
   CMVE_REQUIRE(h, "cmve_dist_destroy: NULL handle");
   dist_release(h);

@@ -76,9 +76,10 @@ __device__ __forceinline__ bool pack_bf(const EvalSide& A, const EvalCommon& c) 
   return !(c.mode == CMVE_SIM_F16 && A.h16 != nullptr);
 }
 __device__ __forceinline__ void pack_bounds(const EvalSide& A, int64_t row, double inv, bool bf, double e1, double e2,
-                                            double e3, int lane, float (&eb)[3]) {
+                                            double e3, int lane, float (&eb)[3], double e4 = 0.0) {
   if (lane == 0) {
     A.inv[row] = inv;
+    if (A.r8) A.err_r8[row] = f32_round_up(sqrt(e4) * (1.0 + 1e-9) + 1e-12);  // (r8_elem's residuals)
     // pack_row_planes' bounds
     eb[0] = bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY;
     eb[1] = bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY;
@@ -97,7 +98,8 @@ __device__ __forceinline__ void pack_regs(const EvalSide& A, const EvalCommon& c
   pack_regs_lane(A, c, row, v, inv, lane, acc);
   const bool bf = pack_bf(A, c);
   const double e1 = bf ? wave_sum(acc.e1) : 0.0, e2 = bf ? wave_sum(acc.e2) : 0.0, e3 = wave_sum(acc.e3);
-  pack_bounds(A, row, inv, bf, e1, e2, e3, lane, eb);
+  const double e4 = A.r8 ? wave_sum(acc.e4) : 0.0;
+  pack_bounds(A, row, inv, bf, e1, e2, e3, lane, eb, e4);
 }
 
 __device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalCommon& c, int64_t row,
@@ -108,12 +110,15 @@ __device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalComm
   const bool want_f16 = frow != nullptr;
   if (c.mode == CMVE_SIM_F16 && want_f16) {
     // the F16 rank GEMM reads only the fp16 plane: the bf16 planes are not written and their bounds
-    // are +inf (a stale plane can never pass for a bounded one)
+    // are +inf (a stale plane can never pass for a bounded one); with A.r8 the 8-bit residual plane of the
+    // level-2 re-score is written beside it (r8_elem)
+    int8_t* rrow = A.r8 ? A.r8 + row * c.d_pad : nullptr;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int64_t k = (int64_t)lane * 4 + 256 * m;
       if (k >= c.d_pad) break;
       cmve_u16x4 fv = {0, 0, 0, 0};
+      uint32_t rv = 0u;
       if (k < c.d) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -122,9 +127,15 @@ __device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalComm
           const double r3 = xh - (double)hf16;
           acc.e3 = fma(r3, r3, acc.e3);
           fv[q] = __builtin_bit_cast(uint16_t, hf16);
+          if (rrow) {
+            double e4;
+            rv |= (uint32_t)(uint8_t)r8_elem(r3, fv[q], e4) << (8 * q);
+            acc.e4 = fma(e4, e4, acc.e4);
+          }
         }
       }
       *(cmve_u16x4*)(frow + k) = fv;
+      if (rrow) *(uint32_t*)(rrow + k) = rv;
     }
   } else {
 #pragma unroll
@@ -292,7 +303,7 @@ __device__ __forceinline__ void eval_prep_body(const EvalSide& q, const EvalSide
   const int64_t row = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
   for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
     c.bucket[t] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < 10) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+  if (blockIdx.x == 0 && threadIdx.x < 12) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
   float eb[3] = {0.f, 0.f, 0.f};  // this wave's row bounds (lane 0; padding rows 0)
   if (!(c.dbg & 1)) {
     if (row < q.n_pad)
@@ -338,7 +349,7 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
   const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
   for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
     c.bucket[t] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < 10) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+  if (blockIdx.x == 0 && threadIdx.x < 12) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
   float ebq[3] = {0.f, 0.f, 0.f}, ebg[3] = {0.f, 0.f, 0.f};
   if (i < q.n_pad && !(c.dbg & 1)) {
     if (i >= q.n) {  // padding rows of both sides: zero vectors, zero bounds, never counted
@@ -359,10 +370,29 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
         }
       }
     } else {
-      const int64_t p = q.idx[q.off[i]];
+      // the caller asserts a one-to-one pairing; it is checked here (t2v(i) = [p], p a real video, v2t(p) = [i])
+      // so that lists which are not one write nothing of side g: the row's video is never touched by two waves
+      // or out of range.  Such a row gets an empty GT list (q.sgt NaN) and gt1 = -2, which the finish counts
+      // into stats[11] (the host mirror raises on it)
+      const int64_t qb = q.off[i];
+      const int64_t p0 = q.off[i + 1] - qb == 1 ? (int64_t)q.idx[qb] : -1;
+      const int64_t p = p0 >= 0 && p0 < g.n ? p0 : 0;  // (row 0 is a real row: loaded, never written when invalid)
       double v[4][4], w[4][4];
       load_row_regs((const TQ*)q.raw + i * q.ld, c.d, lane, v);
       load_row_regs((const TG*)g.raw + p * g.ld, c.d, lane, w);
+      const int64_t gb = g.off[p];
+      const bool valid = p0 == p && g.off[p + 1] - gb == 1 && (int64_t)g.idx[gb] == i;
+      if (!valid) {
+        double e[1] = {lane_sumsq(v, c.d, lane)};
+        wave_sum_k<1>(e);
+        const double invq = row_inv_norm(e[0], q.eps, q.flags);
+        pack_regs(q, c, i, v, invq, lane, ebq);
+        if (lane == 0) {
+          q.sgt[i] = (double)NAN;
+          q.cnt[i] = 0;
+          if (q.gt1) q.gt1[i] = -2;
+        }
+      } else {
       // both norms and the pair's dot in one butterfly, then both planes' residual sums in another (each sum
       // in wave_sum's order: the bits of the separate reductions)
       double r3[3] = {lane_sumsq(v, c.d, lane), lane_sumsq(w, c.d, lane), lane_dot(v, w, c.d, lane)};
@@ -372,11 +402,11 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
       pack_regs_lane(q, c, i, v, invq, lane, aq);
       pack_regs_lane(g, c, p, w, invg, lane, ag);
       const bool bfq = pack_bf(q, c), bfg = pack_bf(g, c);
-      if (!bfq && !bfg) {  // the F16 rank GEMM's planes: only the fp16 residuals
-        double e[2] = {aq.e3, ag.e3};
-        wave_sum_k<2>(e);
-        pack_bounds(q, i, invq, false, 0.0, 0.0, e[0], lane, ebq);
-        pack_bounds(g, p, invg, false, 0.0, 0.0, e[1], lane, ebg);
+      if (!bfq && !bfg) {  // the F16 rank GEMM's planes: only the fp16 (and r8) residuals
+        double e[4] = {aq.e3, ag.e3, aq.e4, ag.e4};
+        wave_sum_k<4>(e);
+        pack_bounds(q, i, invq, false, 0.0, 0.0, e[0], lane, ebq, e[2]);
+        pack_bounds(g, p, invg, false, 0.0, 0.0, e[1], lane, ebg, e[3]);
       } else {
         double e[6] = {aq.e1, aq.e2, aq.e3, ag.e1, ag.e2, ag.e3};
         wave_sum_k<6>(e);
@@ -391,6 +421,7 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
         g.cnt[p] = 0;
         if (q.gt1) q.gt1[i] = (int32_t)p;
         if (g.gt1) g.gt1[p] = (int32_t)i;
+      }
       }
     }
   }
@@ -484,10 +515,14 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
   const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t rq = 0, rg = 0;
+  bool unpaired = false;  // a CMVE_EVAL_PAIRED row whose lists were not a one-to-one pairing (the paired prep)
   if (q.off && i < q.n) {
     rq = gt_rank_of(q.cnt[i], q.sgt[i], g.n);
     q.ranks[i] = rq;
+    unpaired = q.gt1 && q.gt1[i] == -2;
   }
+  const unsigned long long unp = __builtin_amdgcn_ballot_w64(unpaired);
+  if (unp && lane == 0) atomicAdd((unsigned long long*)&c.stats[11], (unsigned long long)__builtin_popcountll(unp));
   if (g.off && i < g.n) {
     rg = gt_rank_of(g.cnt[i], g.sgt[i], q.n);
     g.ranks[i] = rg;

@@ -32,6 +32,8 @@ struct EvalSide {
   int64_t* ranks;      // out: 1-based ranks of this direction
   int32_t* gt1;        // the first GT of each row (idx[off[row]], -1: none / padding), written by the prep: the
                        // rank GEMM drops that GT pair from the undecided list (it can never be counted)
+  int8_t* r8;          // F16 rank path: [n_pad, d_pad] 8-bit residual plane of x_hat - h16 (r8_elem), nullptr: off
+  float* err_r8;       // [n_pad] upper bound of ||x_hat - (h16 + r8 residual)||_2 (the level-2 re-score's bound)
 };
 
 struct EvalCommon {

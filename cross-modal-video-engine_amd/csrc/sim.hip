@@ -99,7 +99,66 @@ struct SimArgs {
   int64_t q_ld, g_ld, d;
   const double* q_inv;
   const double* g_inv;
+  // K14 level-2 re-score (F16 rank path): the 8-bit residual planes the prep wrote beside the fp16 planes (qhi /
+  // ghi) and their per-row bounds; a band pair is decided from h16 + r8 (r8_value) when its score clears the
+  // GT score by the level-2 bound, and re-scored in fp64 only otherwise.  nullptr: every pair in fp64
+  const int8_t* q_r8;
+  const int8_t* g_r8;
+  const float* q_e8;
+  const float* g_e8;
 };
+
+// ---- K14 level-2 re-score: one pair's score from the fp16 + r8 planes (r8_elem, cmve_internal.h) ----
+// lane L holds elements [16L, 16L + 16) of each 1024-element chunk: two 16-B fp16 loads and one 16-B r8 load
+// per row and chunk.  Every element x2 is exact in fp32 and every product exact in fp64, so the fp64 sum's
+// error is a few ulps of 1: |s2 - cos64| <= e8_q + (1 + e8_q) e8_g + 2e-12 (the 2e-12 covers the fp64 sums here
+// and in cos64, as score_error_bound's 1e-12 does for the MFMA bound)
+struct R8Frag {
+  uint4 h0, h1, r;
+};
+__device__ __forceinline__ void r8_load(const uint16_t* __restrict__ hrow, const int8_t* __restrict__ rrow,
+                                        int64_t k, R8Frag& f) {
+  f.h0 = *(const uint4*)(hrow + k);
+  f.h1 = *(const uint4*)(hrow + k + 8);
+  f.r = *(const uint4*)(rrow + k);
+}
+__device__ __forceinline__ double r8_partial(const R8Frag& a, const R8Frag& b, double acc) {
+  const uint32_t ah[8] = {a.h0.x, a.h0.y, a.h0.z, a.h0.w, a.h1.x, a.h1.y, a.h1.z, a.h1.w};
+  const uint32_t bh[8] = {b.h0.x, b.h0.y, b.h0.z, b.h0.w, b.h1.x, b.h1.y, b.h1.z, b.h1.w};
+  const uint32_t ar[4] = {a.r.x, a.r.y, a.r.z, a.r.w}, br[4] = {b.r.x, b.r.y, b.r.z, b.r.w};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const uint16_t ha = (uint16_t)(ah[e >> 1] >> (16 * (e & 1))), hb = (uint16_t)(bh[e >> 1] >> (16 * (e & 1)));
+    const int8_t ra = (int8_t)(ar[e >> 2] >> (8 * (e & 3))), rb = (int8_t)(br[e >> 2] >> (8 * (e & 3)));
+    acc = fma((double)r8_value(ha, ra), (double)r8_value(hb, rb), acc);
+  }
+  return acc;
+}
+// the wave's level-2 scores of P pairs (rows qr[p] of the query planes, gc[p] of the gallery planes), every
+// load of all P pairs in flight before the sums; d_pad % 64 == 0 (a lane's 16 elements are all in or all out)
+template <int P>
+__device__ __forceinline__ void r8_scores(const SimArgs& a, const int64_t (&qr)[P], const int64_t (&gc)[P], int lane,
+                                          double (&s2)[P]) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) s2[p] = 0.0;
+  for (int64_t k0 = 0; k0 < a.ldk; k0 += 1024) {
+    const int64_t k = k0 + 16 * lane;
+    if (k < a.ldk) {
+      R8Frag fq[P], fg[P];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        r8_load(a.qhi + qr[p] * a.ldk, a.q_r8 + qr[p] * a.ldk, k, fq[p]);
+        r8_load(a.ghi + gc[p] * a.ldk, a.g_r8 + gc[p] * a.ldk, k, fg[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) s2[p] = r8_partial(fq[p], fg[p], s2[p]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int p = 0; p < P; ++p) s2[p] += __shfl_xor(s2[p], o, 64);
+}
 
 // bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
 // block id -> its XCD's contiguous share of [0, total): XCD x (= bid & 7) walks its own range in dispatch order
@@ -309,6 +368,9 @@ struct EpiLds<BM, BN, false, INL> {
 #endif
 #ifndef CMVE_BATCH_FIX1
 #define CMVE_BATCH_FIX1 1
+#endif
+#ifndef CMVE_R8_P
+#define CMVE_R8_P 2  // K14 level-2 re-score: pairs per wave in flight at once
 #endif
 // BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): the block picks the problem's
 // argument block in `tab` (see batch_item below); otherwise `tab` is unused
@@ -804,6 +866,46 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
 #endif
           if (listed) {
             CMVE_BAR_LDS();
+            if (a.q_r8) {
+              // level 2: each wave scores CMVE_R8_P listed pairs at once from the fp16 + r8 planes (r8_scores) and
+              // decides every direction whose GT score lies outside s2 +- E2; the directions left undecided stay in
+              // the entry's flags for the fp64 pass below (the wave owns its entries: no other wave touches them)
+              constexpr int RP = CMVE_R8_P;
+              for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
+                int64_t qr[RP], gc[RP];
+                uint32_t ent[RP];
+#pragma unroll
+                for (int u = 0; u < RP; ++u) {
+                  ent[u] = p0 + u < ntot ? epi.list[p0 + u] : epi.list[p0];  // (a repeat: scored, not used)
+                  qr[u] = m0 + (ent[u] & 0xff);
+                  gc[u] = n0 + ((ent[u] >> 8) & 0xff);
+                }
+                double s2[RP];
+                r8_scores<RP>(a, qr, gc, lane, s2);
+                if (lane == 0) {
+#pragma unroll
+                  for (int u = 0; u < RP; ++u) {
+                    if (p0 + u >= ntot) break;
+                    const double eq = (double)a.q_e8[qr[u]], eg = (double)a.g_e8[gc[u]];
+                    const double E2 = eq + (1.0 + eq) * eg + 2e-12;
+                    uint32_t fl = (ent[u] >> 16) & 3u;
+                    const int lr = (int)(ent[u] & 0xff), lc = (int)((ent[u] >> 8) & 0xff);
+                    if (fl & 1u) {
+                      const double t = epi.sgt[lr];
+                      if (s2[u] - E2 > t) { lds_add_u32_async(&lds_rc[lr], 1); fl &= ~1u; }
+                      else if (s2[u] + E2 < t) fl &= ~1u;
+                    }
+                    if (fl & 2u) {
+                      const double t = epi.sgt[BM + lc];
+                      if (s2[u] - E2 > t) { lds_add_u32_async(&lds_cc[lc], 1); fl &= ~2u; }
+                      else if (s2[u] + E2 < t) fl &= ~2u;
+                    }
+                    epi.list[p0 + u] = (ent[u] & 0xffffu) | (fl << 16);
+                  }
+                }
+              }
+              CMVE_BAR_LDS();  // the level-2 flags are in LDS for every wave
+            }
             auto rescore2 = [&](uint32_t e1, uint32_t e2, bool two) {
               const int64_t r1 = m0 + (e1 & 0xff), c1 = n0 + ((e1 >> 8) & 0xff);
               const int64_t r2 = two ? m0 + (e2 & 0xff) : r1, c2 = two ? n0 + ((e2 >> 8) & 0xff) : c1;
@@ -846,6 +948,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
             if constexpr (FIX1) {
               for (int p = wave; p < ntot; p += NW) {
                 const uint32_t e = epi.list[p];
+                if (!(e >> 16)) continue;  // decided at level 2
                 const int64_t r1 = m0 + (e & 0xff), c1 = n0 + ((e >> 8) & 0xff);
                 const double inva = a.q_inv[r1], invb = a.g_inv[c1];
                 double s1;
@@ -862,6 +965,11 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                   if ((e >> 16) & 1u) { if (s1 > epi.sgt[r1 - m0]) lds_add_u32_async(&lds_rc[r1 - m0], 1); }
                   if ((e >> 17) & 1u) { if (s1 > epi.sgt[BM + c1 - n0]) lds_add_u32_async(&lds_cc[c1 - n0], 1); }
                 }
+              }
+            } else if (a.q_r8) {  // level 3 after level 2: the few pairs left, one at a time per wave
+              for (int p = wave; p < ntot; p += NW) {
+                const uint32_t e = epi.list[p];
+                if (e >> 16) rescore2(e, 0u, false);
               }
             } else {
               for (int p = 2 * wave; p < ntot; p += 2 * NW)
@@ -1710,9 +1818,10 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
 
 namespace {
 struct EvalWs {
-  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, q_gt1, g_gt1, cand, total;
+  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, q_gt1, g_gt1, q_e8, g_e8, q_r8, g_r8, cand, total;
 };
-EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
+// (the r8 planes: [n_pad, d_pad] int8 each side, the level-2 re-score's residuals; r8_elem)
+EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t d_pad, int64_t cand_cap) {
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   EvalWs w;
   size_t o = 0;
@@ -1738,6 +1847,14 @@ EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t cand_cap) {
   o = up(o + 4 * (size_t)nq_pad);
   w.g_gt1 = o;
   o = up(o + 4 * (size_t)ng_pad);
+  w.q_e8 = o;
+  o = up(o + 4 * (size_t)nq_pad);
+  w.g_e8 = o;
+  o = up(o + 4 * (size_t)ng_pad);
+  w.q_r8 = o;
+  o = up(o + (size_t)nq_pad * (size_t)d_pad);
+  w.g_r8 = o;
+  o = up(o + (size_t)ng_pad * (size_t)d_pad);
   w.cand = o;
   o = up(o + 8 * (size_t)cand_cap);
   w.total = o;
@@ -1758,7 +1875,7 @@ extern "C" int cmve_eval_debug_stamps(void* host, int64_t bytes) {
 extern "C" int cmve_eval_workspace(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int64_t* bytes) {
   CMVE_REQUIRE(q && g && bytes, "cmve_eval_workspace: NULL argument");
   CMVE_REQUIRE(cand_cap > 0, "cmve_eval_workspace: cand_cap must be > 0");
-  *bytes = (int64_t)eval_ws_layout(q->n_pad, g->n_pad, cand_cap).total;
+  *bytes = (int64_t)eval_ws_layout(q->n_pad, g->n_pad, q->d_pad, cand_cap).total;
   return CMVE_OK;
 }
 
@@ -1851,7 +1968,7 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
                "%s: GT offsets and indices go together", fn);
   CMVE_REQUIRE(row_off || col_off, "%s: no direction requested", fn);
   CMVE_REQUIRE(ws && out, "%s: NULL workspace / output", fn);
-  const EvalWs w = eval_ws_layout(q->n_pad, g->n_pad, cand_cap);
+  const EvalWs w = eval_ws_layout(q->n_pad, g->n_pad, q->d_pad, cand_cap);
   CMVE_REQUIRE(cand_cap > 0 && ws_bytes >= (int64_t)w.total, "%s: workspace has %lld bytes, needs %lld", fn,
                (long long)ws_bytes, (long long)w.total);
   CandLayout l = cand_layout(g->n_pad, cand_cap);
@@ -1938,6 +2055,22 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   const char* fix_env = getenv("CMVE_EVAL_FIX_LAUNCH");  // kernel studies / tests: the separate fix-up launch
   const bool no_inline = fix_env && atoi(fix_env) != 0;
   P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
+  // level-2 re-score from the fp16 + r8 planes: the F16 mode whose prep runs the register path (the only one
+  // that writes r8: 16-B row pieces, d_pad <= 1024, both sides); CMVE_EVAL_NO_R8 (tests / kernel studies) off
+  static const bool no_r8 = [] {
+    const char* e = getenv("CMVE_EVAL_NO_R8");
+    return e && atoi(e) != 0;
+  }();
+  if (P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_r8) {
+    P.sq.r8 = (int8_t*)(base + w.q_r8);
+    P.sg.r8 = (int8_t*)(base + w.g_r8);
+    P.sq.err_r8 = (float*)(base + w.q_e8);
+    P.sg.err_r8 = (float*)(base + w.g_e8);
+    a.q_r8 = P.sq.r8;
+    a.g_r8 = P.sg.r8;
+    a.q_e8 = P.sq.err_r8;
+    a.g_e8 = P.sg.err_r8;
+  }
   if (P.inline_fix) {
     a.fix_inline = 1;
     a.q_f64 = P.qf;

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 17
+#define CMVE_ABI_VERSION 18
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -396,7 +396,13 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
  * mode may carry CMVE_EVAL_PAIRED: the caller asserts a one-to-one GT pairing -- every t2v list is one
  * video p = row_idx[row_off[i]], every v2t list is one caption, and v2t(p) = [i] (MSR-VTT-1kA's
  * structure; q->n == g->n) -- and launch 1 then packs and scores each (caption, video) pair in one wave
- * (half the row reads; same results bit for bit).  Lists that are not such a pairing give undefined ranks.
+ * (half the row reads; same results bit for bit).  Launch 1 checks the assertion per caption (t2v(i) = [p],
+ * 0 <= p < g->n, v2t(p) = [i]); a caption that fails it writes nothing of side g, ranks as if its list
+ * were empty and is counted in out[11] (0 for a true pairing): with out[11] != 0 the ranks are undefined,
+ * but no write leaves the workspace / planes and no row is written by two waves.
+ * At F16 size with d_pad <= 1024 and 16-B aligned rows the workspace also holds an 8-bit residual plane of
+ * each side (x_hat - fp16 plane, in 1/256 ulps of the fp16 element): launch 2 decides a band pair from
+ * fp16 + residual (error <= e8_q + (1 + e8_q) e8_g, ~2e-6) and re-scores in fp64 only the pairs within that.
  */
 #define CMVE_EVAL_TIMING_SLOTS 32
 #define CMVE_EVAL_PAIRED 0x100
@@ -480,6 +486,16 @@ int cmve_dist_reduce_rank(cmve_handle_t h, double* best_gt, int32_t* counts, int
 int cmve_dist_allgather_topk(cmve_handle_t h, const int64_t* ids, const double* scores, int64_t n_q, int32_t k,
                              int64_t* gathered_ids, double* gathered_scores, int32_t k_out, int64_t* out_ids,
                              double* out_scores);
+/* plain collectives on the handle's stream (dtype CMVE_F32 / F64 / I32 / I64): in-place all-reduce
+ * (op CMVE_DIST_SUM / CMVE_DIST_MAX) of `count` elements, and all-gather of `count` elements per rank into
+ * gathered[nranks * count] in rank order -- the two-direction exchange's int64 SUM (t2v counts, v2t R@K sums,
+ * overflow flag) and the layout / v2t-rank gathers of cmve/dist.py's ShardedGallery over this communicator
+ * (CAbiComm).  cmve_dist_size: the communicator's size and this handle's rank. */
+#define CMVE_DIST_SUM 0
+#define CMVE_DIST_MAX 1
+int cmve_dist_allreduce(cmve_handle_t h, void* buf, int64_t count, int32_t dtype, int32_t op);
+int cmve_dist_allgather(cmve_handle_t h, const void* local, int64_t count, int32_t dtype, void* gathered);
+int cmve_dist_size(cmve_handle_t h, int32_t* nranks, int32_t* rank);
 int cmve_dist_destroy(cmve_handle_t h);
 
 /*

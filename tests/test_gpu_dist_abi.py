@@ -63,3 +63,51 @@ def test_dist_c_abi_single_rank(torch_cuda):
         assert b"no communicator" in _lib.lib.cmve_last_error()
     finally:
         _lib.check(_lib.lib.cmve_dist_destroy(h), "cmve_dist_destroy")
+
+
+def test_sharded_gallery_over_c_abi_comm(torch_cuda):
+    """ShardedGallery's two-direction evaluation, cal_perf and top-k driven through CAbiComm (the C ABI's RCCL
+    communicator: cmve_dist_allreduce / cmve_dist_allgather / cmve_dist_size, run even at world 1) against the
+    same calls over the default communicator and the oracle: identical ranks, tuples and top-k lists; the
+    plain collectives reject unsupported dtypes."""
+    import numpy as np
+    import torch
+    from cmve import _lib
+    from cmve.dist import CAbiComm, ShardedGallery
+    from oracle import retrieval as R
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(44)
+    n, nq, d = 2500, 1800, 256
+    v = rng.standard_normal((n, d)).astype(np.float32)
+    gt = rng.integers(0, n, nq)
+    c = (v[gt] + 1.3 * rng.standard_normal((nq, d))).astype(np.float32)
+    t2v = [[int(g)] for g in gt]
+    v2t = [[] for _ in range(n)]
+    for i, g in enumerate(gt):
+        v2t[int(g)].append(i)
+    comm = CAbiComm(dev)
+    try:
+        assert (comm.rank, comm.world) == (0, 1)
+        a = ShardedGallery(torch.from_numpy(v).to(dev), offset=0, n_global=n, device=dev, comm=comm)
+        b = ShardedGallery(torch.from_numpy(v).to(dev), offset=0, n_global=n, device=dev)
+        qt = torch.from_numpy(c).to(dev)
+        ra, va = a.evaluate(qt, t2v, v2t)
+        rb, vb = b.evaluate(qt, t2v, v2t)
+        s = R.exact_scores64(c, v)
+        assert np.array_equal(ra, rb) and np.array_equal(va, vb)
+        assert np.array_equal(ra, R.rank_counts(s, t2v)) and np.array_equal(va, R.rank_counts(s.T, v2t))
+        t2v_d = {i: l for i, l in enumerate(t2v)}
+        assert a.cal_perf(qt, v2t, t2v_d) == b.cal_perf(qt, v2t, t2v_d)
+        ia, sa = a.topk(qt, 10)
+        ib, sb = b.topk(qt, 10)
+        assert np.array_equal(ia, ib) and np.array_equal(sa, sb)
+        with pytest.raises(ValueError):
+            comm.all_reduce(torch.zeros(4, dtype=torch.int16, device=dev), "sum")
+        x = torch.arange(6, dtype=torch.int64, device=dev)
+        comm.all_reduce(x, "max")
+        out = torch.empty(6, dtype=torch.int64, device=dev)
+        comm.all_gather_into(out, x)
+        torch.cuda.synchronize()
+        assert x.tolist() == list(range(6)) and out.tolist() == list(range(6))
+    finally:
+        comm.close()

@@ -835,3 +835,71 @@ def test_rank_batch_stream_outs_timing(golden, torch_cuda):
         ms = b.kernel_timing(0)
         assert ms[0] > 0 and ms[1] > 0 and ms[2] == 0 and ms[3] > 0
         b.close()
+
+
+def _dense_inputs(noise, paired, seed=91, n=1000, d=256, k=160):
+    """160 near-duplicate captions / videos (one vector + `noise`): every pair among them lies inside the fp16
+    band.  noise 1e-4: their scores ~1e-8 apart, inside the level-2 (fp16 + r8) band too, so they reach the fp64
+    pass; noise 3e-3: ~1e-5 apart, mostly decided at level 2, some at its bound's edge."""
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal((n, d))
+    v[:k] = v[0] + noise * rng.standard_normal((k, d))
+    c = v + 0.8 * rng.standard_normal((n, d))
+    c[:k] = v[0] + noise * rng.standard_normal((k, d))
+    t2v = [[i] for i in range(n)]
+    v2t = [[j] for j in range(n)] if paired else [[j, (j + 1) % n] if j % 3 == 0 else [j] for j in range(n)]
+    return c, v, t2v, v2t
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("noise", [3e-3, 1e-5])
+def test_level2_rescore_near_ties(torch_cuda, noise):
+    """The K14 level-2 re-score (fp16 + 8-bit residual planes, bound e8_q + (1 + e8_q) e8_g) at its bound's scale:
+    160 near-duplicate rows whose pair scores differ by ~1e-5 (3e-3 noise: decided at level 2, some within a few
+    bounds) or ~1e-10 (1e-5 noise: every such pair falls through to fp64).  Ranks == the oracle's exact counts in
+    both directions, paired prep."""
+    import torch
+    from cmve import engine
+    c, v, t2v, v2t = _dense_inputs(noise, True, seed=17)
+    n, d = c.shape
+    s = R.exact_scores64(c, v)
+    sess = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64)
+    r, cc = sess.run(torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    assert np.array_equal(r, R.rank_counts(s, t2v)) and np.array_equal(cc, R.rank_counts(s.T, v2t))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["paired_f16", "multi_gt_f16", "paired_bf16x3"])
+def test_rank_batch_dense_tiles(torch_cuda, case):
+    """RankBatch over tiles dense with undecided pairs (the batch geometries: 128 x 128 for fp16 / bf16, 128 x 64
+    for split-bf16): the tiles over the 160 near-duplicates hold more pairs than the 1,024-entry LDS list, so they
+    take the per-wave re-score (lr / lc decoding of WN = 2 / TM = 2 / TN = 4); the others the list, level 2 and
+    fp64.  Every output word equals each session's own evaluation and the oracle's exact counts; the pair total
+    shows the dense tiles went past the list."""
+    import torch
+    from cmve import engine, _lib
+    paired = case.startswith("paired")
+    mode = _lib.SIM_BF16X3 if case.endswith("bf16x3") else _lib.SIM_F16
+    sets, exp = [], []
+    for j, noise in enumerate((1e-4, 3e-3, 1e-4)):
+        c, v, t2v, v2t = _dense_inputs(noise, paired, seed=91 + j)
+        s = R.exact_scores64(c, v)
+        exp.append((R.rank_counts(s, t2v), R.rank_counts(s.T, v2t)))
+        sets.append((torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda()))
+    n, d = sets[0][0].shape
+    ref = []
+    for cq, gv in sets:
+        s_ = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64, mode=mode)
+        s_.run(cq, gv)
+        ref.append(s_.out.clone())
+    sess = [engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64, mode=mode) for _ in sets]
+    assert sess[0].paired == paired
+    b = engine.RankBatch(sess, sets)
+    b.run()
+    torch.cuda.synchronize()
+    for s_, r_, (er, ec) in zip(sess, ref, exp):
+        h = s_.out.cpu().numpy()
+        assert torch.equal(s_.out, r_)
+        assert h[9] == 0 and h[8] > 4 * 1024  # no overflow; the dense tiles went past the LDS list
+        assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)
+    b.close()
