@@ -575,13 +575,15 @@ class ShardedGallery:
 
     # ---- both directions (cal_perf) ----
     def evaluate_device(self, q_all: torch.Tensor, row_csr, col_csr, n_q: int, mode: int = _lib.SIM_F16,
-                        events=None):
+                        events=None, q=None):
         """One exact two-direction evaluation of the gathered captions against every shard, no host
         synchronisation.  row_csr: t2v GT lists restricted to this shard (``local_gt_csr``) or None;
         col_csr: this shard's v2t GT lists into the gathered captions (``local_v2t_csr``) or None.
         Returns (t2v ranks int64 [n_q] | None -- global, equal on every rank; v2t ranks int64 [n] | None
-        -- this shard's videos; v2t recall sums int64 [4] | None -- all shards; overflow bool [])."""
-        q = self._pack(q_all, mode)
+        -- this shard's videos; v2t recall sums int64 [4] | None -- all shards; overflow bool []).  q: the
+        captions already packed (``_pack(q_all, mode)``), reused across passes over the same captions."""
+        if q is None:
+            q = self._pack(q_all, mode)
         sgt_r = merge_gt_scores(self._row_gt(q, row_csr, mode), self.comm) if row_csr is not None else None
         col = self._col_gt(q, col_csr, mode) if (col_csr is not None and self.n > 0) else None
         rc, cc, ovf = self._count(q, mode, sgt_r, col, events=events)
@@ -607,11 +609,15 @@ class ShardedGallery:
         (global) of gathered caption i; v2t_gts[v] = GT caption ids (gathered order) of global video v.
         Returns (t2v ranks [n_q] | None, v2t ranks [n_global] | None)."""
         q_all = all_gather_var(q_local, self.comm)
+        return self._evaluate_gathered(q_all, self._pack(q_all, mode), t2v_gts, v2t_gts, mode)
+
+    def _evaluate_gathered(self, q_all, q, t2v_gts, v2t_gts, mode: int):
+        """evaluate() on captions already gathered (q_all) and packed (q)."""
         n_q = q_all.shape[0]
         row_csr = self.local_gt_csr(t2v_gts) if t2v_gts is not None else None
         col_csr = self.local_v2t_csr(v2t_gts) if v2t_gts is not None else None
         for _attempt in range(4):
-            t2v, v2t, _, ovf = self.evaluate_device(q_all, row_csr, col_csr, n_q, mode)
+            t2v, v2t, _, ovf = self.evaluate_device(q_all, row_csr, col_csr, n_q, mode, q=q)
             if not bool(ovf.item()):
                 break
             self._grow()
@@ -643,22 +649,24 @@ class ShardedGallery:
         n_global videos of GT caption ids (gathered order); t2v_gt: dict or list over the captions of GT
         video ids (metrics.get_gt's outputs).  t2v mAP is the AP of each caption's FIRST GT
         (metrics.py:61-79); v2t mAP is over every GT caption of a video (metrics.py:83-102)."""
+        # the captions are gathered and packed ONCE; every pass below (both directions, the first-GT t2v pass, the
+        # v2t GT positions) reuses them
         q_all = all_gather_var(q_local, self.comm)
         n_q = q_all.shape[0]
+        q = self._pack(q_all, mode)
         t2v_lists = [t2v_gt[i] for i in range(n_q)]  # KeyError on a caption without GT, like metrics.py:142
         v2t_lists = [v2t_gt[j] for j in range(self.n_global)]
-        t2v, v2t = self.evaluate(q_local, t2v_lists, v2t_lists, mode)
+        t2v, v2t = self._evaluate_gathered(q_all, q, t2v_lists, v2t_lists, mode)
         firsts = [[l[0]] for l in t2v_lists]
         if all(len(l) == 1 for l in t2v_lists):
             t2v_first = t2v
         else:
-            t2v_first, _ = self.evaluate(q_local, firsts, None, mode)
+            t2v_first, _ = self._evaluate_gathered(q_all, q, firsts, None, mode)
         t2v_map = float(np.mean(1.0 / t2v_first))
         local = self.local_v2t_lists(v2t_lists)
         if all(len(l) <= 1 for l in v2t_lists):
             aps = [1.0 / v2t[self.offset + j] if local[j] else 0.0 for j in range(self.n)]
         else:
-            q = self._pack(q_all, mode)
             aps = [ap_from_positions(p) for p in self._positions(q, local, mode)]
         s = torch.tensor([float(np.sum(aps))], dtype=torch.float64, device=self.device)
         v2t_map = float(reduce_counts(s, self.comm).item()) / self.n_global

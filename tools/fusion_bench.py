@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--nq", type=int, default=30364)
     ap.add_argument("--nv", type=int, default=44493)
     ap.add_argument("--chunk", type=int, default=8192, help="rows per combine_batches call (multiple of 32)")
-    ap.add_argument("--loop-q", type=int, default=2048, help="queries timed through the per-batch loop")
+    ap.add_argument("--loop-q", type=int, default=30364,
+                    help="queries run through the per-batch loop (timed; and compared with combine_batches)")
+    ap.add_argument("--sample", type=int, default=256, help="queries whose target ranks are checked in fp64")
     print(json.dumps(run(ap.parse_args())))
 
 
@@ -45,6 +47,7 @@ def run(a):
     mid = torch.randn((a.nq, 8, 16, 640), generator=gen, device=dev)
     ref = torch.randint(0, a.nv, (a.nq,), generator=gen, device=dev)
     tgt = (ref + torch.randint(1, a.nv, (a.nq,), generator=gen, device=dev)) % a.nv
+    tgt[::97] = ref[::97]  # a target equal to its reference: removed with it, never retrieved (rank 0)
     out = {"nq": a.nq, "nv": a.nv, "dims": [640, 2560, 5120], "batch": 32,
            "gflop_per_query": flops_per_query() / 1e9}
 
@@ -61,9 +64,10 @@ def run(a):
     torch.cuda.synchronize()
     # (a) the reference's loop structure: one combine_features call per batch of 32
     nl = min(a.loop_q, a.nq) // 32 * 32
+    if nl < a.nq and a.loop_q >= a.nq:
+        nl = a.nq  # every query, the last partial batch included (validate.py:207-208 in file order)
     t0 = time.perf_counter()
-    for i in range(0, nl, 32):
-        m.combine_features((high[i:i + 32], mid[i:i + 32]), text[i:i + 32])
+    loop_outs = [m.combine_features((high[i:i + 32], mid[i:i + 32]), text[i:i + 32]) for i in range(0, nl, 32)]
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out["loop_per_batch"] = {"queries": nl, "ms": dt * 1e3, "queries_per_s": nl / dt}
@@ -80,9 +84,12 @@ def run(a):
     out["combine_batches"] = {"chunk": chunk, "ms": dt_c * 1e3, "queries_per_s": a.nq / dt_c,
                               "tflops_algorithmic": fl / dt_c / 1e12,
                               "note": "GEMMs run split-bf16 (3 MFMAs per product) for the 1e-5 parity bar"}
-    same = torch.equal(pred[:nl], V.normalize(torch.cat(
-        [m.combine_features((high[i:i + 32], mid[i:i + 32]), text[i:i + 32]) for i in range(0, nl, 32)])))
+    loop_out = torch.cat(loop_outs)
+    del loop_outs
+    same = torch.equal(pred[:loop_out.shape[0]], V.normalize(loop_out))
     out["combine_batches"]["identical_to_loop"] = bool(same)
+    out["combine_batches"]["queries_compared_with_loop"] = int(loop_out.shape[0])
+    del loop_out
     # (c) exact target ranks with reference removal (validate.py:71-138)
     names = list(range(a.nv))
     refs, tgts = ref.tolist(), tgt.tolist()
@@ -100,6 +107,23 @@ def run(a):
                                               for k in (1, 5, 10, 50)]}
     total = dt_c + dt_r
     out["end_to_end"] = {"ms": total * 1e3, "queries_per_s": a.nq / total}
+    # (d) an independent fp64 scoring of a sample of queries (torch fp64 GEMM, not the fused path): the rank of
+    # the target among the gallery with the reference removed, validate.py:76-87 -- 1 + #{j != ref : s_j > s_t},
+    # 0 when target == reference -- must equal the fused path's rank for every sampled query
+    ns = min(a.sample, a.nq)
+    idx = torch.linspace(0, a.nq - 1, ns, device=dev).round().long()
+    s64 = pred[idx].double() @ pooled.double().T
+    ar = torch.arange(ns, device=dev)
+    st = s64[ar, tgt[idx]]
+    better = (s64 > st[:, None])
+    better[ar, ref[idx]] = False
+    want = better.sum(1) + 1
+    want = torch.where(tgt[idx] == ref[idx], torch.zeros_like(want), want).cpu().numpy()
+    got = ranks[idx.cpu().numpy()]
+    out["ranking"]["fp64_sample"] = {"queries": ns, "mismatches": int(np.count_nonzero(got != want)),
+                                     "reference_above_target": int((s64[ar, ref[idx]] > st).sum().item()),
+                                     "target_is_reference": int((tgt[idx] == ref[idx]).sum().item())}
+    out["ranking"]["zero_rank_iff_target_is_reference"] = bool(np.array_equal(ranks == 0, (tgt == ref).cpu().numpy()))
     return out
 
 

@@ -24,5 +24,6 @@ A="$HB --inflight 1 --no-replay --steps 20 --warmup 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/trace" -o run -- python3 "$R/bench.py" $A > "$R/$O/trace.log" 2>&1 || { echo "trace failed"; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/$O/fetch" -o run -- python3 "$R/bench.py" $A > "$R/$O/fetch.log" 2>&1 || { echo "fetch failed"; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$R/$O/write" -o run -- python3 "$R/bench.py" $A > "$R/$O/write.log" 2>&1 || { echo "write failed"; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d "$R/$O/sq" -o run -- python3 "$R/bench.py" $A > "$R/$O/sq.log" 2>&1 || echo "sq pass failed (continuing)"
 python3 "$R/tools/traffic_1ka.py" "$R/$O" $TAG > "$R/$O/traffic.log" 2>&1
 tail -c 2500 "$R/$O/traffic.log"
