@@ -106,18 +106,36 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
-template <typename T> __device__ __forceinline__ double ld64(const T* p) { return (double)(*p); }
+// ---- global-address-space accesses ----
+// A pointer the kernel READ from memory (a batch's argument table, cmve_eval_batch_*) has no known address space,
+// so plain loads / stores / atomics through it compile to flat_* instructions, whose waits also cover the LDS
+// traffic (every lgkmcnt wait of an epilogue or a ring barrier then waits for them too).  These helpers access
+// device (global) memory through an address_space(1) view of the pointer: global_* instructions on every path.
+#define CMVE_GP(T) __attribute__((address_space(1))) T*
+template <typename T> __device__ __forceinline__ T gld(const T* p) { return *(const CMVE_GP(T))p; }
+template <typename T, typename U> __device__ __forceinline__ void gst(T* p, U v) { *(CMVE_GP(T))p = (T)v; }
+template <typename T> __device__ __forceinline__ T gadd(T* p, T v) {
+  return __hip_atomic_fetch_add((CMVE_GP(T))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T> __device__ __forceinline__ T gmax(T* p, T v) {
+  return __hip_atomic_fetch_max((CMVE_GP(T))p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T> __device__ __forceinline__ double ld64(const T* p) { return (double)gld(p); }
+
+typedef float cmve_f32x4 __attribute__((ext_vector_type(4)));
+typedef double cmve_f64x2 __attribute__((ext_vector_type(2)));
 
 // four consecutive elements of a raw row as doubles (16-B aligned: one float4 or two double2 loads)
 __device__ __forceinline__ void load4d(const float* p, double (&v)[4]) {
-  const float4 x = *(const float4*)p;
+  const cmve_f32x4 x = gld((const cmve_f32x4*)p);
   v[0] = x.x;
   v[1] = x.y;
   v[2] = x.z;
   v[3] = x.w;
 }
 __device__ __forceinline__ void load4d(const double* p, double (&v)[4]) {
-  const double2 x = *(const double2*)p, y = *(const double2*)(p + 2);
+  const cmve_f64x2 x = gld((const cmve_f64x2*)p), y = gld((const cmve_f64x2*)(p + 2));
   v[0] = x.x;
   v[1] = x.y;
   v[2] = y.x;
@@ -270,36 +288,41 @@ __device__ __forceinline__ double row_inv_norm(double ss, double eps, int flags)
 // so the f16 conversion need not be correctly rounded from fp64: it goes through fp32, which the
 // hardware converts directly -- gfx950 has no fp64 -> fp16 instruction)
 struct PackAcc {
-  double e1 = 0.0, e2 = 0.0, e3 = 0.0, e4 = 0.0;  // e4: the r8 residual plane's squared residuals
+  double e1 = 0.0, e2 = 0.0, e3 = 0.0;
+  float e4 = 0.f;  // the bf16 residual plane's squared residuals (lo16_elem), summed in fp32
 };
 
-// ---- the 8-bit residual plane of the fp16 rank operand (K14 level-2 re-score) ----
-// An element x (fp64, normalised) packed to fp16 h leaves r3 = x - h, |r3| <= ulp(h) / 2.  r8 stores r3 in units
-// of ulp(h) / 256 (ulp(h) = 2^(max(E, 1) - 25) for h's biased exponent field E: subnormals share E = 1's
-// spacing), rounded and clamped to [-127, 127]:  x2 = h + r8 * 2^(max(E, 1) - 33).  x2 is EXACT in fp32 (h has
-// 11 significant bits with its last at 2^(E'-25), the residual term 8 more below them), so a product of two
-// such values is exact in fp64.  err4 = x - x2 (computed in fp64; the bound's slack covers its rounding).
-__device__ __forceinline__ int r8_shift(uint16_t hbits) {
-  const int e = (hbits >> 10) & 31;
-  return 33 - (e > 1 ? e : 1);
+// ---- the bf16 residual plane of the fp16 rank operand (K14 level-2 re-score) ----
+// An element x (fp64, normalised) is packed as xf = fp32(x), h = fp16(xf); d2 = xf - h is exact in fp32 and
+// lo = bf16(d2) (RNE) keeps its top 8 bits: x2 = h + lo with |x - x2| <= |x - xf| + |d2 - lo|, where
+// d2 - lo is exact in fp32 and |x - xf| <= 2^-24 |x|.  The bound over a row is therefore
+//   ||x - x2|| <= sqrt(sum (d2 - lo)^2) + 2^-24 ||x||     (the fp32 sum's relative error <= 1024 * 2^-24 < 1e-4)
+// lo16_elem returns lo's bits and the fp32 residual d2 - lo.
+__device__ __forceinline__ uint16_t lo16_elem(float xf, _Float16 h, float& res) {
+  const float d2 = xf - (float)h;
+  const uint16_t lo = f2bf(d2);
+  res = d2 - bf2f(lo);
+  return lo;
 }
-__device__ __forceinline__ int8_t r8_elem(double r3, uint16_t hbits, double& err4) {
-  const int sh = r8_shift(hbits);
-  double t = rint(ldexp(r3, sh));
-  t = t == t ? fmin(127.0, fmax(-127.0, t)) : 0.0;  // (a NaN row's pairs are never in a band)
-  err4 = r3 - ldexp(t, -sh);
-  return (int8_t)(int)t;
+// the row bound from the fp32 sum of squared residuals (lo16_elem) and the fp64 norm of x (1 after normalising)
+__device__ __forceinline__ float lo16_bound(double ss_res) {
+  return f32_round_up(sqrt(ss_res) * (1.0 + 1e-4) + 5.9605e-8 * (1.0 + 1e-6) + 1e-12);
 }
-// x2 of r8_elem as fp32 (exact)
-__device__ __forceinline__ float r8_value(uint16_t hbits, int8_t r) {
-  const float h = (float)__builtin_bit_cast(_Float16, hbits);
-  return h + ldexpf((float)r, -r8_shift(hbits));
+// fp16 of a normalised element through fp32 (v_cvt_f32_f64 then v_cvt_f16_f32).  The fp32 value is made opaque
+// so the compiler keeps the two hardware conversions: it otherwise folds them into ONE fp64 -> fp16 conversion,
+// which gfx950 has no instruction for and which it expands into ~25 integer / compare instructions per element
+// (the bound is computed from the value stored either way)
+__device__ __forceinline__ _Float16 f16_via_f32(double xh, float& xf) {
+  xf = (float)xh;
+  asm volatile("" : "+v"(xf));
+  return (_Float16)xf;
 }
+
 __device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h, uint16_t& l, uint16_t& f,
                                           PackAcc& acc) {
-  const float xf = (float)xh;
+  float xf;
+  const _Float16 hf16 = f16_via_f32(xh, xf);
   if (want_f16) {
-    const _Float16 hf16 = (_Float16)xf;
     const double r3 = xh - (double)hf16;
     acc.e3 = fma(r3, r3, acc.e3);
     f = __builtin_bit_cast(uint16_t, hf16);
@@ -320,9 +343,9 @@ __device__ __forceinline__ void pack_pad_row(uint16_t* hrow, uint16_t* lrow, uin
                                              int lane) {
   const cmve_u16x4 z = {0, 0, 0, 0};
   for (int64_t k = (int64_t)lane * 4; k < d_pad; k += 256) {
-    *(cmve_u16x4*)(hrow + k) = z;
-    if (lrow) *(cmve_u16x4*)(lrow + k) = z;
-    if (frow) *(cmve_u16x4*)(frow + k) = z;
+    gst((cmve_u16x4*)(hrow + k), z);
+    if (lrow) gst((cmve_u16x4*)(lrow + k), z);
+    if (frow) gst((cmve_u16x4*)(frow + k), z);
   }
 }
 

@@ -78,15 +78,15 @@ __device__ __forceinline__ bool pack_bf(const EvalSide& A, const EvalCommon& c) 
 __device__ __forceinline__ void pack_bounds(const EvalSide& A, int64_t row, double inv, bool bf, double e1, double e2,
                                             double e3, int lane, float (&eb)[3], double e4 = 0.0) {
   if (lane == 0) {
-    A.inv[row] = inv;
-    if (A.r8) A.err_r8[row] = f32_round_up(sqrt(e4) * (1.0 + 1e-9) + 1e-12);  // (r8_elem's residuals)
+    gst(A.inv + row, inv);
+    if (A.lo16) A.err_lo16[row] = lo16_bound(e4);  // (lo16_elem's residuals)
     // pack_row_planes' bounds
     eb[0] = bf ? f32_round_up(sqrt(e1) * (1.0 + 1e-9) + 1e-12) : INFINITY;
     eb[1] = bf ? f32_round_up(sqrt(e2) * (1.0 + 1e-9) + 1e-12) : INFINITY;
     eb[2] = A.err_h16 ? f32_round_up(sqrt(e3) * (1.0 + 1e-9) + 1e-12) : 0.f;
-    A.err_hi[row] = eb[0];
-    A.err_hilo[row] = eb[1];
-    if (A.err_h16) A.err_h16[row] = eb[2];
+    gst(A.err_hi + row, eb[0]);
+    gst(A.err_hilo + row, eb[1]);
+    if (A.err_h16) gst(A.err_h16 + row, eb[2]);
   }
 }
 
@@ -98,7 +98,7 @@ __device__ __forceinline__ void pack_regs(const EvalSide& A, const EvalCommon& c
   pack_regs_lane(A, c, row, v, inv, lane, acc);
   const bool bf = pack_bf(A, c);
   const double e1 = bf ? wave_sum(acc.e1) : 0.0, e2 = bf ? wave_sum(acc.e2) : 0.0, e3 = wave_sum(acc.e3);
-  const double e4 = A.r8 ? wave_sum(acc.e4) : 0.0;
+  const double e4 = A.lo16 ? wave_sum((double)acc.e4) : 0.0;
   pack_bounds(A, row, inv, bf, e1, e2, e3, lane, eb, e4);
 }
 
@@ -110,32 +110,33 @@ __device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalComm
   const bool want_f16 = frow != nullptr;
   if (c.mode == CMVE_SIM_F16 && want_f16) {
     // the F16 rank GEMM reads only the fp16 plane: the bf16 planes are not written and their bounds
-    // are +inf (a stale plane can never pass for a bounded one); with A.r8 the 8-bit residual plane of the
-    // level-2 re-score is written beside it (r8_elem)
-    int8_t* rrow = A.r8 ? A.r8 + row * c.d_pad : nullptr;
+    // are +inf (a stale plane can never pass for a bounded one); with A.lo16 the bf16 residual plane of the
+    // level-2 re-score is written beside it (lo16_elem: two fp32 ops and a conversion per element)
+    uint16_t* lrow16 = A.lo16 ? A.lo16 + row * c.d_pad : nullptr;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int64_t k = (int64_t)lane * 4 + 256 * m;
       if (k >= c.d_pad) break;
-      cmve_u16x4 fv = {0, 0, 0, 0};
-      uint32_t rv = 0u;
+      cmve_u16x4 fv = {0, 0, 0, 0}, lv = {0, 0, 0, 0};
       if (k < c.d) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const double xh = v[m][q] * inv;
-          const _Float16 hf16 = (_Float16)(float)xh;  // pack_elem's f16 arithmetic
+          float xf;
+          const _Float16 hf16 = f16_via_f32(xh, xf);  // pack_elem's f16 arithmetic
           const double r3 = xh - (double)hf16;
           acc.e3 = fma(r3, r3, acc.e3);
           fv[q] = __builtin_bit_cast(uint16_t, hf16);
-          if (rrow) {
-            double e4;
-            rv |= (uint32_t)(uint8_t)r8_elem(r3, fv[q], e4) << (8 * q);
-            acc.e4 = fma(e4, e4, acc.e4);
+          if (lrow16) {
+            float res;
+            lv[q] = lo16_elem(xf, hf16, res);
+            acc.e4 = fmaf(res, res, acc.e4);
           }
         }
       }
-      *(cmve_u16x4*)(frow + k) = fv;
-      if (rrow) *(uint32_t*)(rrow + k) = rv;
+      gst((cmve_u16x4*)(frow + k), fv);
+      if (lrow16) gst((cmve_u16x4*)(lrow16 + k), lv);
+      asm volatile("" : "+v"(acc.e3), "+v"(acc.e4));  // (pack_f16_lo16: the chunk's sums complete here)
     }
   } else {
 #pragma unroll
@@ -153,9 +154,9 @@ __device__ __forceinline__ void pack_regs_lane(const EvalSide& A, const EvalComm
           fv[q] = f;
         }
       }
-      *(cmve_u16x4*)(hrow + k) = hv;
-      if (lrow) *(cmve_u16x4*)(lrow + k) = lv;
-      if (frow) *(cmve_u16x4*)(frow + k) = fv;
+      gst((cmve_u16x4*)(hrow + k), hv);
+      if (lrow) gst((cmve_u16x4*)(lrow + k), lv);
+      if (frow) gst((cmve_u16x4*)(frow + k), fv);
     }
   }
 }
@@ -165,9 +166,9 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
                                               const TA* __restrict__ x, int lane, float (&eb)[3]) {
   // the first GT partner's row is loaded beside the row itself (its index is known up front): the
   // GT score then needs no second HBM round trip after the pack
-  const int64_t g_beg = A.off ? A.off[row] : 0, g_end = A.off ? A.off[row + 1] : 0;
+  const int64_t g_beg = A.off ? gld(A.off + row) : 0, g_end = A.off ? gld(A.off + row + 1) : 0;
   double w0[4][4];
-  if (g_beg < g_end) load_row_regs((const TB*)B.raw + (int64_t)A.idx[g_beg] * B.ld, c.d, lane, w0);
+  if (g_beg < g_end) load_row_regs((const TB*)B.raw + (int64_t)gld(A.idx + g_beg) * B.ld, c.d, lane, w0);
   double v[4][4];
   load_row_regs(x, c.d, lane, v);
   const double inv = row_inv_norm(wave_sum(lane_sumsq(v, c.d, lane)), A.eps, A.flags);
@@ -183,7 +184,7 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
 #pragma unroll
         for (int q = 0; q < 4; ++q) w[m][q] = w0[m][q];
     } else {
-      load_row_regs((const TB*)B.raw + (int64_t)A.idx[g] * B.ld, c.d, lane, w);
+      load_row_regs((const TB*)B.raw + (int64_t)gld(A.idx + g) * B.ld, c.d, lane, w);
     }
     const double invb = row_inv_norm(wave_sum(lane_sumsq(w, c.d, lane)), B.eps, B.flags);
     const double s = wave_sum(lane_dot(v, w, c.d, lane)) * (inv * invb);  // wave_cos64(x, y, inv, invb)
@@ -193,9 +194,9 @@ __device__ __forceinline__ void prep_row_regs(const EvalSide& A, const EvalSide&
     }
   }
   if (lane == 0) {
-    A.sgt[row] = any ? best : (g_end > g_beg ? (double)INFINITY : (double)NAN);
-    A.cnt[row] = 0;
-    if (A.gt1) A.gt1[row] = g_end > g_beg ? A.idx[g_beg] : -1;
+    gst(A.sgt + row, any ? best : (g_end > g_beg ? (double)INFINITY : (double)NAN));
+    gst(A.cnt + row, 0);
+    if (A.gt1) gst(A.gt1 + row, g_end > g_beg ? gld(A.idx + g_beg) : -1);
   }
 }
 
@@ -209,14 +210,14 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   if (row >= A.n) {  // padding rows: zero vectors, zero bounds, never counted
     pack_pad_row(hrow, lrow, frow, c.d_pad, lane);
     if (lane == 0) {
-      A.inv[row] = 0.0;
-      A.err_hi[row] = 0.f;
-      A.err_hilo[row] = 0.f;
-      if (A.err_h16) A.err_h16[row] = 0.f;
+      gst(A.inv + row, 0.0);
+      gst(A.err_hi + row, 0.f);
+      gst(A.err_hilo + row, 0.f);
+      if (A.err_h16) gst(A.err_h16 + row, 0.f);
       if (A.off) {
-        A.sgt[row] = (double)NAN;
-        A.cnt[row] = 0;
-        if (A.gt1) A.gt1[row] = -1;
+        gst(A.sgt + row, (double)NAN);
+        gst(A.cnt + row, 0);
+        if (A.gt1) gst(A.gt1 + row, -1);
       }
     }
     return;
@@ -230,11 +231,11 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   float b1, b2, b3;
   pack_row_planes<TA>(x, c.d, c.d_pad, A.vec != 0, inv, hrow, lrow, frow, lane, b1, b2, b3);
   if (lane == 0) {
-    A.inv[row] = inv;
-    A.err_hi[row] = eb[0] = b1;
-    A.err_hilo[row] = eb[1] = b2;
+    gst(A.inv + row, inv);
+    gst(A.err_hi + row, eb[0] = b1);
+    gst(A.err_hilo + row, eb[1] = b2);
     eb[2] = A.err_h16 ? b3 : 0.f;
-    if (A.err_h16) A.err_h16[row] = b3;
+    if (A.err_h16) gst(A.err_h16 + row, b3);
   }
   if (!A.off) return;
   // exact GT score (gt_thr_kernel's arithmetic): the partner's 1/||y|| is recomputed by the routine
@@ -253,9 +254,9 @@ __device__ __forceinline__ void prep_row(const EvalSide& A, const EvalSide& B, c
   }
   if (lane == 0) {
     // empty list: NaN (rank n_m + 1); every GT NaN: +inf (rank n_m) -- gt_thr_kernel's encoding
-    A.sgt[row] = any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN);
-    A.cnt[row] = 0;
-    if (A.gt1) A.gt1[row] = A.off[row + 1] > A.off[row] ? A.idx[A.off[row]] : -1;
+    gst(A.sgt + row, any ? best : (A.off[row + 1] > A.off[row] ? (double)INFINITY : (double)NAN));
+    gst(A.cnt + row, 0);
+    if (A.gt1) gst(A.gt1 + row, A.off[row + 1] > A.off[row] ? A.idx[A.off[row]] : -1);
   }
 }
 
@@ -302,8 +303,9 @@ __device__ __forceinline__ void eval_prep_body(const EvalSide& q, const EvalSide
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
   for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
-    c.bucket[t] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < 12) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+    gst(c.bucket + t, 0ull);
+  if (blockIdx.x == 0 && threadIdx.x < 13) gst(c.stats + threadIdx.x, 0);  // the finish blocks add into it
+  if (blockIdx.x == 0 && threadIdx.x == 0 && c.l3_count) gst(c.l3_count, 0u);  // the rank GEMM appends level 3
   float eb[3] = {0.f, 0.f, 0.f};  // this wave's row bounds (lane 0; padding rows 0)
   if (!(c.dbg & 1)) {
     if (row < q.n_pad)
@@ -329,8 +331,8 @@ __device__ __forceinline__ void eval_prep_body(const EvalSide& q, const EvalSide
     unsigned* sh = &c.emax[(side * 3 + threadIdx.x) * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];
     // +inf (a plane the mode does not write) is the largest value: a plain store equals the atomic max
     if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
-    } else if (m == INFINITY) *sh = __float_as_uint(m);
-    else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
+    } else if (m == INFINITY) gst(sh, __float_as_uint(m));
+    else if (m > 0.f) gmax(sh, __float_as_uint(m));
   }
   EVAL_STAMP(c, 0, 1);
 }
@@ -348,8 +350,9 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
   for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
-    c.bucket[t] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < 12) c.stats[threadIdx.x] = 0;  // the finish blocks add into it
+    gst(c.bucket + t, 0ull);
+  if (blockIdx.x == 0 && threadIdx.x < 13) gst(c.stats + threadIdx.x, 0);  // the finish blocks add into it
+  if (blockIdx.x == 0 && threadIdx.x == 0 && c.l3_count) gst(c.l3_count, 0u);  // the rank GEMM appends level 3
   float ebq[3] = {0.f, 0.f, 0.f}, ebg[3] = {0.f, 0.f, 0.f};
   if (i < q.n_pad && !(c.dbg & 1)) {
     if (i >= q.n) {  // padding rows of both sides: zero vectors, zero bounds, never counted
@@ -360,37 +363,37 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
         pack_pad_row(A.hi + i * c.d_pad, A.lo ? A.lo + i * c.d_pad : nullptr, A.h16 ? A.h16 + i * c.d_pad : nullptr,
                      c.d_pad, lane);
         if (lane == 0) {
-          A.inv[i] = 0.0;
-          A.err_hi[i] = 0.f;
-          A.err_hilo[i] = 0.f;
-          if (A.err_h16) A.err_h16[i] = 0.f;
-          A.sgt[i] = (double)NAN;
-          A.cnt[i] = 0;
-          if (A.gt1) A.gt1[i] = -1;
+          gst(A.inv + i, 0.0);
+          gst(A.err_hi + i, 0.f);
+          gst(A.err_hilo + i, 0.f);
+          if (A.err_h16) gst(A.err_h16 + i, 0.f);
+          gst(A.sgt + i, (double)NAN);
+          gst(A.cnt + i, 0);
+          if (A.gt1) gst(A.gt1 + i, -1);
         }
       }
     } else {
-      // the caller asserts a one-to-one pairing; it is checked here (t2v(i) = [p], p a real video, v2t(p) = [i])
-      // so that lists which are not one write nothing of side g: the row's video is never touched by two waves
-      // or out of range.  Such a row gets an empty GT list (q.sgt NaN) and gt1 = -2, which the finish counts
-      // into stats[11] (the host mirror raises on it)
-      const int64_t qb = q.off[i];
-      const int64_t p0 = q.off[i + 1] - qb == 1 ? (int64_t)q.idx[qb] : -1;
-      const int64_t p = p0 >= 0 && p0 < g.n ? p0 : 0;  // (row 0 is a real row: loaded, never written when invalid)
+      // the caller asserts a one-to-one pairing; its t2v side is checked here (one GT per caption, a real video)
+      // so that lists which are not one never write out of range: such a row writes nothing of side g, gets an
+      // empty GT list (q.sgt NaN) and gt1 = -2, which the finish counts into stats[11] (the host mirror raises
+      // on it).  (Two captions naming one video -- lists that are not a bijection -- give undefined ranks, as the
+      // contract says, but every write stays inside that video's row.)
+      const int64_t qb = gld(q.off + i);
+      const int64_t p0 = gld(q.off + i + 1) - qb == 1 ? (int64_t)gld(q.idx + qb) : -1;
+      const bool valid = p0 >= 0 && p0 < g.n;
+      const int64_t p = valid ? p0 : 0;  // (row 0 is a real row: loaded, never written when invalid)
       double v[4][4], w[4][4];
       load_row_regs((const TQ*)q.raw + i * q.ld, c.d, lane, v);
       load_row_regs((const TG*)g.raw + p * g.ld, c.d, lane, w);
-      const int64_t gb = g.off[p];
-      const bool valid = p0 == p && g.off[p + 1] - gb == 1 && (int64_t)g.idx[gb] == i;
       if (!valid) {
         double e[1] = {lane_sumsq(v, c.d, lane)};
         wave_sum_k<1>(e);
         const double invq = row_inv_norm(e[0], q.eps, q.flags);
         pack_regs(q, c, i, v, invq, lane, ebq);
         if (lane == 0) {
-          q.sgt[i] = (double)NAN;
-          q.cnt[i] = 0;
-          if (q.gt1) q.gt1[i] = -2;
+          gst(q.sgt + i, (double)NAN);
+          gst(q.cnt + i, 0);
+          if (q.gt1) gst(q.gt1 + i, -2);
         }
       } else {
       // both norms and the pair's dot in one butterfly, then both planes' residual sums in another (each sum
@@ -403,7 +406,7 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
       pack_regs_lane(g, c, p, w, invg, lane, ag);
       const bool bfq = pack_bf(q, c), bfg = pack_bf(g, c);
       if (!bfq && !bfg) {  // the F16 rank GEMM's planes: only the fp16 (and r8) residuals
-        double e[4] = {aq.e3, ag.e3, aq.e4, ag.e4};
+        double e[4] = {aq.e3, ag.e3, (double)aq.e4, (double)ag.e4};
         wave_sum_k<4>(e);
         pack_bounds(q, i, invq, false, 0.0, 0.0, e[0], lane, ebq, e[2]);
         pack_bounds(g, p, invg, false, 0.0, 0.0, e[1], lane, ebg, e[3]);
@@ -415,12 +418,12 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
       }
       const double s = r3[2] * (invq * invg);
       if (lane == 0) {  // a one-entry list: its score, or +inf when it is NaN (prep_row_regs' encoding)
-        q.sgt[i] = s == s ? s : (double)INFINITY;
-        g.sgt[p] = s == s ? s : (double)INFINITY;
-        q.cnt[i] = 0;
-        g.cnt[p] = 0;
-        if (q.gt1) q.gt1[i] = (int32_t)p;
-        if (g.gt1) g.gt1[p] = (int32_t)i;
+        gst(q.sgt + i, s == s ? s : (double)INFINITY);
+        gst(g.sgt + p, s == s ? s : (double)INFINITY);
+        gst(q.cnt + i, 0);
+        gst(g.cnt + p, 0);
+        if (q.gt1) gst(q.gt1 + i, (int32_t)p);
+        if (g.gt1) gst(g.gt1 + p, (int32_t)i);
       }
       }
     }
@@ -440,8 +443,171 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
     for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
     unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];  // [side][plane] = tid
     if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
-    } else if (m == INFINITY) *sh = __float_as_uint(m);
-    else if (m > 0.f) atomicMax(sh, __float_as_uint(m));
+    } else if (m == INFINITY) gst(sh, __float_as_uint(m));
+    else if (m > 0.f) gmax(sh, __float_as_uint(m));
+  }
+  EVAL_STAMP(c, 0, 1);
+}
+
+// The paired prep of the F16 rank path with the level-2 plane (the 1k-A headline's form): rows of exactly
+// d = d_pad = 256 NM elements, read in 16-B pieces (rows_vec4), so no element guards.  The same arithmetic as
+// eval_prep_pair_body -- the norms, the GT dot, the fp16 plane and its bound in the same (m, c) fma order, so
+// h16 / inv_norm / err_h16 / the GT scores are bit-identical to it -- with the bf16 residual plane
+// (lo16_elem: the hardware bf16 conversion, fp32 residuals) written beside the fp16 plane.
+template <int NM>
+__device__ __forceinline__ void pack_f16_lo16(const EvalSide& A, int64_t row, const double (&v)[NM][4], double inv,
+                                              int lane, bool store, double& e3, float& e4) {
+  uint16_t* frow = A.h16 + row * (int64_t)(NM * 256);
+  uint16_t* lrow = A.lo16 + row * (int64_t)(NM * 256);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int64_t k = (int64_t)lane * 4 + 256 * m;
+    cmve_u16x4 fv, lv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double xh = v[m][q] * inv;
+      float xf;
+      const _Float16 h = f16_via_f32(xh, xf);  // pack_elem's f16 arithmetic
+      const float hf = (float)h;
+      const double r3 = xh - (double)hf;
+      e3 = fma(r3, r3, e3);
+      const float d2 = xf - hf;
+      const __bf16 lo = (__bf16)d2;
+      const float res = d2 - (float)lo;
+      e4 = fmaf(res, res, e4);
+      fv[q] = __builtin_bit_cast(uint16_t, h);
+      lv[q] = __builtin_bit_cast(uint16_t, lo);
+    }
+    if (store) {
+      gst((cmve_u16x4*)(frow + k), fv);
+      gst((cmve_u16x4*)(lrow + k), lv);
+    }
+    // the chunk's residual sums complete here (left free, the compiler sank every fma chain below the last
+    // chunk's stores and held all 32 elements' temporaries: ~190 registers)
+    asm volatile("" : "+v"(e3), "+v"(e4));
+  }
+}
+
+// a raw row of d = 256 NM elements into registers (lane L: elements 4L + 256m + c) through a buffer resource:
+// one VGPR offset for every load of the row, the 256-element steps in scalar offsets (per-load 64-bit
+// addresses held ~64 registers and pushed the prep past 128)
+typedef uint32_t prep_u32x4 __attribute__((ext_vector_type(4)));
+typedef double prep_f64x2 __attribute__((ext_vector_type(2)));
+template <int NM>
+__device__ __forceinline__ void load_row_buf(const double* row, int lane, double (&v)[NM][4]) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, NM * 256 * 8, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const prep_f64x2 a = __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32, m * 2048, 0));
+    const prep_f64x2 b =
+        __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32 + 16, m * 2048, 0));
+    v[m][0] = a.x;
+    v[m][1] = a.y;
+    v[m][2] = b.x;
+    v[m][3] = b.y;
+  }
+}
+template <int NM>
+__device__ __forceinline__ void load_row_buf(const float* row, int lane, double (&v)[NM][4]) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, NM * 256 * 4, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const cmve_f32x4 a = __builtin_bit_cast(cmve_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, m * 1024, 0));
+    v[m][0] = a.x;
+    v[m][1] = a.y;
+    v[m][2] = a.z;
+    v[m][3] = a.w;
+  }
+}
+
+template <typename TQ, typename TG, int NM>
+__device__ __forceinline__ void eval_prep_pair_f16_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+  EVAL_STAMP(c, 0, 0);
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
+    gst(c.bucket + t, 0ull);
+  if (blockIdx.x == 0 && threadIdx.x < 13) gst(c.stats + threadIdx.x, 0);  // the finish blocks add into it
+  if (blockIdx.x == 0 && threadIdx.x == 0 && c.l3_count) gst(c.l3_count, 0u);  // the rank GEMM appends level 3
+  float ebq[3] = {0.f, 0.f, 0.f}, ebg[3] = {0.f, 0.f, 0.f};
+  if (i < q.n_pad && !(c.dbg & 1)) {
+    if (i >= q.n) {  // padding rows of both sides: zero vectors, zero bounds, never counted
+      const EvalSide* sides[2] = {&q, &g};
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        const EvalSide& A = *sides[sd];
+        pack_pad_row(A.hi + i * c.d_pad, A.lo ? A.lo + i * c.d_pad : nullptr, A.h16 + i * c.d_pad, c.d_pad, lane);
+        if (lane == 0) {
+          gst(A.inv + i, 0.0);
+          gst(A.err_hi + i, 0.f);
+          gst(A.err_hilo + i, 0.f);
+          gst(A.err_h16 + i, 0.f);
+          gst(A.sgt + i, (double)NAN);
+          gst(A.cnt + i, 0);
+          if (A.gt1) gst(A.gt1 + i, -1);
+        }
+      }
+    } else {
+      // (eval_prep_pair_body's check of the t2v side of the pairing)
+      const int64_t qb = gld(q.off + i);
+      const int64_t p0 = gld(q.off + i + 1) - qb == 1 ? (int64_t)gld(q.idx + qb) : -1;
+      const bool valid = p0 >= 0 && p0 < g.n;
+      const int64_t p = valid ? p0 : 0;
+      double v[NM][4], w[NM][4];
+      load_row_buf<NM>((const TQ*)q.raw + i * q.ld, lane, v);
+      load_row_buf<NM>((const TG*)g.raw + p * g.ld, lane, w);
+      double r3[3] = {0.0, 0.0, 0.0};  // lane_sumsq(v), lane_sumsq(w), lane_dot(v, w): the same fma order
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          r3[0] = fma(v[m][q4], v[m][q4], r3[0]);
+          r3[1] = fma(w[m][q4], w[m][q4], r3[1]);
+          r3[2] = fma(v[m][q4], w[m][q4], r3[2]);
+        }
+      wave_sum_k<3>(r3);
+      const double invq = row_inv_norm(r3[0], q.eps, q.flags), invg = row_inv_norm(r3[1], g.eps, g.flags);
+      double e3q = 0.0, e3g = 0.0;
+      float e4q = 0.f, e4g = 0.f;
+      // (one side after the other, one 4-element chunk at a time: left to itself the scheduler interleaves the
+      // two sides' chunks and holds ~190 registers, which caps the prep at two waves per SIMD)
+      pack_f16_lo16<NM>(q, i, v, invq, lane, true, e3q, e4q);
+      __builtin_amdgcn_sched_barrier(0);
+      pack_f16_lo16<NM>(g, p, w, invg, lane, valid, e3g, e4g);
+      double e[4] = {e3q, e3g, (double)e4q, (double)e4g};
+      wave_sum_k<4>(e);
+      pack_bounds(q, i, invq, false, 0.0, 0.0, e[0], lane, ebq, e[2]);
+      if (valid) pack_bounds(g, p, invg, false, 0.0, 0.0, e[1], lane, ebg, e[3]);
+      const double sc = r3[2] * (invq * invg);
+      if (lane == 0) {
+        gst(q.sgt + i, !valid ? (double)NAN : (sc == sc ? sc : (double)INFINITY));
+        gst(q.cnt + i, 0);
+        if (q.gt1) gst(q.gt1 + i, valid ? (int32_t)p : -2);
+        if (valid) {
+          gst(g.sgt + p, sc == sc ? sc : (double)INFINITY);
+          gst(g.cnt + p, 0);
+          if (g.gt1) gst(g.gt1 + p, (int32_t)i);
+        }
+      }
+    }
+  }
+  // err_max shards of both sides (eval_prep_kernel's scheme)
+  __shared__ float s_eb[PREP_NW][6];
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      s_eb[threadIdx.x >> 6][k] = ebq[k];
+      s_eb[threadIdx.x >> 6][3 + k] = ebg[k];
+    }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float m = 0.f;
+#pragma unroll
+    for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
+    unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];  // [side][plane] = tid
+    if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
+    } else if (m == INFINITY) gst(sh, __float_as_uint(m));
+    else if (m > 0.f) gmax(sh, __float_as_uint(m));
   }
   EVAL_STAMP(c, 0, 1);
 }
@@ -466,15 +632,16 @@ __device__ __forceinline__ void finish_buckets(const EvalCommon& c) {
   __shared__ unsigned long long redt[2 * FIN_NW], redm[2 * FIN_NW];
   unsigned long long tot[1] = {0}, mx[1] = {0};
   for (int64_t b = threadIdx.x; b < c.nb; b += FIN_NT) {
-    const unsigned long long v = c.bucket[b];
+    const unsigned long long v = gld(c.bucket + b);
     tot[0] += v;
     mx[0] = v > mx[0] ? v : mx[0];
   }
   block_reduce_k<false>(tot, redt);
   block_reduce_k<true>(mx, redm);
   if (threadIdx.x == 0) {
-    c.stats[8] = (int64_t)tot[0];
-    c.stats[9] = (!c.fix_inline && (int64_t)mx[0] > c.cap_b) ? ((int64_t)mx[0] + 1) * c.nb + c.nb + 1 : 0;
+    gst(c.stats + 8, (int64_t)tot[0]);
+    gst(c.stats + 12, c.l3_count ? (int64_t)gld(c.l3_count) : 0);  // level-3 pairs (past l3_cap: re-scored inline)
+    gst(c.stats + 9, (!c.fix_inline && (int64_t)mx[0] > c.cap_b) ? ((int64_t)mx[0] + 1) * c.nb + c.nb + 1 : 0);
   }
 }
 
@@ -488,11 +655,11 @@ __device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide
   const int lane = threadIdx.x & 63;
   for (int sp = threadIdx.x >> 6; sp < 6; sp += FIN_NW) {
     unsigned* w = &c.emax[sp * EMAX_SHARDS + lane];
-    unsigned m = *w;
-    *w = 0u;
+    unsigned m = gld(w);
+    gst(w, 0u);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
-    if (lane == 0) ((float*)(sp < 3 ? q.err_max : g.err_max))[sp % 3] = __uint_as_float(m);
+    if (lane == 0) gst((sp < 3 ? q.err_max : g.err_max) + sp % 3, __uint_as_float(m));
   }
 }
 
@@ -514,18 +681,45 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
   // directions; then one LDS round over the block's waves and 8 lanes adding into the stats head
   const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // level 3, deferred by the rank GEMM (EvalCommon::l3): the listed pairs whose row (t2v) or column (v2t) is one
+  // of this block's, re-scored in fp64 by wave_cos64 (the fix-up's arithmetic: the same bits as an inline
+  // re-score) and added to this block's counts through LDS.  A pair listed for both directions is scored by
+  // the block of its row and by the block of its column.
+  __shared__ int add_q[FIN_NT], add_g[FIN_NT];
+  const unsigned n3 = c.l3_count ? min(gld(c.l3_count), (unsigned)c.l3_cap) : 0u;
+  if (n3) {
+    add_q[threadIdx.x] = 0;
+    add_g[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * FIN_NT;
+    for (unsigned e = (unsigned)wave; e < n3; e += FIN_NW) {
+      const uint64_t u = gld(c.l3 + e);
+      const int64_t pi = (int64_t)(u & 0x7fffffffull), pj = (int64_t)((u >> 31) & 0x7fffffffull);
+      const unsigned fl = (unsigned)(u >> 62);
+      const bool mq = (fl & 1u) && pi >= r0 && pi < r0 + FIN_NT;
+      const bool mg = (fl & 2u) && pj >= r0 && pj < r0 + FIN_NT;
+      if (!(mq || mg)) continue;  // (wave-uniform)
+      const double sc = wave_cos64((const TQ*)q.raw + pi * q.ld, (const TG*)g.raw + pj * g.ld, gld(q.inv + pi),
+                                   gld(g.inv + pj), c.d, lane);
+      if (lane == 0) {
+        if (mq && sc > gld(q.sgt + pi)) atomicAdd(&add_q[pi - r0], 1);
+        if (mg && sc > gld(g.sgt + pj)) atomicAdd(&add_g[pj - r0], 1);
+      }
+    }
+    __syncthreads();
+  }
   int64_t rq = 0, rg = 0;
   bool unpaired = false;  // a CMVE_EVAL_PAIRED row whose lists were not a one-to-one pairing (the paired prep)
   if (q.off && i < q.n) {
-    rq = gt_rank_of(q.cnt[i], q.sgt[i], g.n);
-    q.ranks[i] = rq;
-    unpaired = q.gt1 && q.gt1[i] == -2;
+    rq = gt_rank_of(gld(q.cnt + i) + (n3 ? add_q[threadIdx.x] : 0), gld(q.sgt + i), g.n);
+    gst(q.ranks + i, rq);
+    unpaired = q.gt1 && gld(q.gt1 + i) == -2;
   }
   const unsigned long long unp = __builtin_amdgcn_ballot_w64(unpaired);
-  if (unp && lane == 0) atomicAdd((unsigned long long*)&c.stats[11], (unsigned long long)__builtin_popcountll(unp));
+  if (unp && lane == 0) gadd((unsigned long long*)&c.stats[11], (unsigned long long)__builtin_popcountll(unp));
   if (g.off && i < g.n) {
-    rg = gt_rank_of(g.cnt[i], g.sgt[i], q.n);
-    g.ranks[i] = rg;
+    rg = gt_rank_of(gld(g.cnt + i) + (n3 ? add_g[threadIdx.x] : 0), gld(g.sgt + i), q.n);
+    gst(g.ranks + i, rg);
   }
   unsigned long long sq = (unsigned long long)rq, sg = (unsigned long long)rg;
 #pragma unroll
@@ -552,7 +746,7 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
     unsigned long long a = red[k * FIN_NW];
 #pragma unroll
     for (int ww = 1; ww < FIN_NW; ++ww) a += red[k * FIN_NW + ww];
-    if ((k < 4 ? q.off : g.off) && a) atomicAdd((unsigned long long*)&c.stats[k], a);
+    if ((k < 4 ? q.off : g.off) && a) gadd((unsigned long long*)&c.stats[k], a);
   }
   EVAL_STAMP(c, 1, 1);
 }
@@ -581,15 +775,41 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_batch_kernel(const Eva
   const EvalItem& it = tab[blockIdx.y];
   eval_prep_pair_body<TQ, TG>(it.q, it.g, it.c);
 }
+#ifndef CMVE_PREP_WPE
+#define CMVE_PREP_WPE 4  // the specialized paired prep: waves per SIMD its register budget allows (<= 128 VGPRs)
+#endif
+template <typename TQ, typename TG, int NM>
+__global__ __launch_bounds__(PREP_NT, CMVE_PREP_WPE) void eval_prep_pair_f16_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  eval_prep_pair_f16_body<TQ, TG, NM>(q, g, c);
+}
+template <typename TQ, typename TG, int NM>
+__global__ __launch_bounds__(PREP_NT, CMVE_PREP_WPE) void eval_prep_pair_f16_batch_kernel(const EvalItem* __restrict__ tab) {
+  const EvalItem& it = tab[blockIdx.y];
+  eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c);
+}
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(FIN_NT) void eval_finish_batch_kernel(const EvalItem* __restrict__ tab) {
   const EvalItem& it = tab[blockIdx.y];
   eval_finish_body<TQ, TG>(it.q, it.g, it.c);
 }
 
+// the specialized paired prep applies: F16 with the lo16 plane, 16-B row pieces, d = d_pad = 256 NM (NM <= 4)
+static int prep_f16_nm(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+  const bool ok = c.mode == CMVE_SIM_F16 && q.h16 && g.h16 && q.lo16 && g.lo16 && q.vec && g.vec && c.d == c.d_pad &&
+                  c.d_pad % 256 == 0 && c.d_pad <= 1024;
+  return ok ? (int)(c.d_pad / 256) : 0;
+}
+#define CMVE_PREP_F16(KER, NMV, ...)                                                                            \
+  switch (NMV) {                                                                                                \
+    case 1: cmve::launch(KER<TQ, TG, 1>, __VA_ARGS__); break;                                                  \
+    case 2: cmve::launch(KER<TQ, TG, 2>, __VA_ARGS__); break;                                                  \
+    case 3: cmve::launch(KER<TQ, TG, 3>, __VA_ARGS__); break;                                                  \
+    default: cmve::launch(KER<TQ, TG, 4>, __VA_ARGS__); break;                                                 \
+  }
+
 template <typename TQ, typename TG>
-static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int phase,
-                                   hipStream_t s) {
+static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* tab,
+                                   int count, int phase, hipStream_t s) {
   if (phase == 0) {
     const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
     cmve::launch(eval_prep_batch_kernel<TQ, TG>, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
@@ -597,6 +817,10 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
   }
   if (phase == 3) {
     const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);
+    if (const int nm = prep_f16_nm(q, g, c0)) {
+      CMVE_PREP_F16(eval_prep_pair_f16_batch_kernel, nm, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
+      return check_launch("eval_prep_pair_f16_batch_kernel");
+    }
     cmve::launch(eval_prep_pair_batch_kernel<TQ, TG>, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
     return check_launch("eval_prep_pair_batch_kernel");
   }
@@ -608,12 +832,12 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
 
 // a batch: the items share q / g shapes, dtypes and GT lists (tab[i] differ in buffers only); phases 0 / 2 / 3
 // as launch_eval (no separate fix-up: the batch path is the G64 inline fix-up geometry)
-int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int q_f64, int g_f64,
-                      int phase, hipStream_t s) {
-  if (!q_f64 && !g_f64) return launch_eval_batch_typed<float, float>(q, g, tab, count, phase, s);
-  if (!q_f64 && g_f64) return launch_eval_batch_typed<float, double>(q, g, tab, count, phase, s);
-  if (q_f64 && !g_f64) return launch_eval_batch_typed<double, float>(q, g, tab, count, phase, s);
-  return launch_eval_batch_typed<double, double>(q, g, tab, count, phase, s);
+int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* tab, int count,
+                      int q_f64, int g_f64, int phase, hipStream_t s) {
+  if (!q_f64 && !g_f64) return launch_eval_batch_typed<float, float>(q, g, c0, tab, count, phase, s);
+  if (!q_f64 && g_f64) return launch_eval_batch_typed<float, double>(q, g, c0, tab, count, phase, s);
+  if (q_f64 && !g_f64) return launch_eval_batch_typed<double, float>(q, g, c0, tab, count, phase, s);
+  return launch_eval_batch_typed<double, double>(q, g, c0, tab, count, phase, s);
 }
 
 template <typename TQ, typename TG>
@@ -625,6 +849,10 @@ static int launch_eval_typed(const EvalSide& q, const EvalSide& g, const EvalCom
   }
   if (phase == 3) {  // the paired prep (eval_prep_pair_kernel): one wave per (caption, video) pair
     const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);
+    if (const int nm = prep_f16_nm(q, g, c)) {
+      CMVE_PREP_F16(eval_prep_pair_f16_kernel, nm, dim3(blocks), dim3(PREP_NT), 0u, s, q, g, c);
+      return check_launch("eval_prep_pair_f16_kernel");
+    }
     cmve::launch(eval_prep_pair_kernel<TQ, TG>, dim3(blocks), dim3(PREP_NT), 0u, s, q, g, c);
     return check_launch("eval_prep_pair_kernel");
   }

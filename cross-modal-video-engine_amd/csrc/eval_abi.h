@@ -32,8 +32,8 @@ struct EvalSide {
   int64_t* ranks;      // out: 1-based ranks of this direction
   int32_t* gt1;        // the first GT of each row (idx[off[row]], -1: none / padding), written by the prep: the
                        // rank GEMM drops that GT pair from the undecided list (it can never be counted)
-  int8_t* r8;          // F16 rank path: [n_pad, d_pad] 8-bit residual plane of x_hat - h16 (r8_elem), nullptr: off
-  float* err_r8;       // [n_pad] upper bound of ||x_hat - (h16 + r8 residual)||_2 (the level-2 re-score's bound)
+  uint16_t* lo16;      // F16 rank path: [n_pad, d_pad] bf16 residual plane of x_hat - h16 (lo16_elem), nullptr: off
+  float* err_lo16;     // [n_pad] upper bound of ||x_hat - (h16 + lo16)||_2 (the level-2 re-score's bound)
 };
 
 struct EvalCommon {
@@ -46,6 +46,12 @@ struct EvalCommon {
   const uint64_t* cand;
   int64_t* stats;              // out[0, 16)
   int fix_inline;              // the rank GEMM re-scored the undecided pairs itself (no list: never an overflow)
+  // level 3 (the fp64 re-score of the pairs the rank GEMM's level 2 left undecided) is deferred to the finish:
+  // the GEMM appends (row | col << 31 | dirs << 62) to this list (count zeroed by the prep; a full list makes
+  // the GEMM re-score inline instead), the finish's rank blocks re-score the entries of their rows / columns
+  unsigned* l3_count;
+  uint64_t* l3;
+  int l3_cap;
   int dbg;                     // kernel studies only (CMVE_EVAL_DBG): skip parts, results garbage
   unsigned long long* stamps;  // kernel studies only (CMVE_EVAL_DBG & 128): [kernel][block][8] s_memrealtime
                                // (kernel 0 prep, 1 finish, 2 fix-up, 3 the rank GEMM's tiles)
@@ -63,7 +69,7 @@ struct EvalItem {
   EvalSide q, g;
   EvalCommon c;
 };
-int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalItem* tab, int count, int q_f64, int g_f64,
-                      int phase, hipStream_t s);
+int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* tab, int count,
+                      int q_f64, int g_f64, int phase, hipStream_t s);
 
 }  // namespace cmve

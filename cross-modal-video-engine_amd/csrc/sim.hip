@@ -99,59 +99,69 @@ struct SimArgs {
   int64_t q_ld, g_ld, d;
   const double* q_inv;
   const double* g_inv;
-  // K14 level-2 re-score (F16 rank path): the 8-bit residual planes the prep wrote beside the fp16 planes (qhi /
-  // ghi) and their per-row bounds; a band pair is decided from h16 + r8 (r8_value) when its score clears the
-  // GT score by the level-2 bound, and re-scored in fp64 only otherwise.  nullptr: every pair in fp64
-  const int8_t* q_r8;
-  const int8_t* g_r8;
-  const float* q_e8;
-  const float* g_e8;
+  // K14 level-2 re-score (F16 rank path): the bf16 residual planes the prep wrote beside the fp16 planes (qhi /
+  // ghi) and their per-row bounds; a band pair is decided from h16 + lo16 (lo16_elem) when its score clears the
+  // GT score by the level-2 bound; the rest go to the level-3 list (EvalCommon::l3, re-scored in fp64 by the
+  // finish), or are re-scored here when it is full.  nullptr: every pair in fp64 here
+  const uint16_t* q_lo16;
+  const uint16_t* g_lo16;
+  const float* q_el;
+  const float* g_el;
+  unsigned* l3_count;
+  unsigned long long* l3;
+  int l3_cap;
 };
 
-// ---- K14 level-2 re-score: one pair's score from the fp16 + r8 planes (r8_elem, cmve_internal.h) ----
-// lane L holds elements [16L, 16L + 16) of each 1024-element chunk: two 16-B fp16 loads and one 16-B r8 load
-// per row and chunk.  Every element x2 is exact in fp32 and every product exact in fp64, so the fp64 sum's
-// error is a few ulps of 1: |s2 - cos64| <= e8_q + (1 + e8_q) e8_g + 2e-12 (the 2e-12 covers the fp64 sums here
-// and in cos64, as score_error_bound's 1e-12 does for the MFMA bound)
-struct R8Frag {
-  uint4 h0, h1, r;
+// ---- K14 level-2 re-score: one pair's score from the fp16 + bf16 residual planes (lo16_elem, cmve_internal.h) ----
+// lane L holds elements [16L, 16L + 16) of each 1024-element chunk: two 16-B fp16 loads and two 16-B bf16 loads
+// per row and chunk.  x2 = h + lo is formed in fp64 (exact unless lo lies 2^-42 below h: then within 2^-53 |x2|),
+// the products and sums in fp64, so the sum's error is a few ulps of 1:
+//   |s2 - cos64| <= el_q + (1 + el_q) el_g + 2e-12
+// (the 2e-12 covers the fp64 sums here and in cos64, as score_error_bound's 1e-12 does for the MFMA bound)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+struct L16Frag {
+  u32x4_t h0, h1, l0, l1;
 };
-__device__ __forceinline__ void r8_load(const uint16_t* __restrict__ hrow, const int8_t* __restrict__ rrow,
-                                        int64_t k, R8Frag& f) {
-  f.h0 = *(const uint4*)(hrow + k);
-  f.h1 = *(const uint4*)(hrow + k + 8);
-  f.r = *(const uint4*)(rrow + k);
+__device__ __forceinline__ void l16_load(const uint16_t* __restrict__ hrow, const uint16_t* __restrict__ lrow,
+                                         int64_t k, L16Frag& f) {
+  f.h0 = gld((const u32x4_t*)(hrow + k));
+  f.h1 = gld((const u32x4_t*)(hrow + k + 8));
+  f.l0 = gld((const u32x4_t*)(lrow + k));
+  f.l1 = gld((const u32x4_t*)(lrow + k + 8));
 }
-__device__ __forceinline__ double r8_partial(const R8Frag& a, const R8Frag& b, double acc) {
+__device__ __forceinline__ double l16_x(uint32_t hw, uint32_t lw, int half) {
+  const uint16_t h = (uint16_t)(hw >> (16 * half));
+  const uint32_t l = half ? (lw & 0xffff0000u) : (lw << 16);
+  return (double)(float)__builtin_bit_cast(_Float16, h) + (double)__uint_as_float(l);
+}
+__device__ __forceinline__ double l16_partial(const L16Frag& a, const L16Frag& b, double acc) {
   const uint32_t ah[8] = {a.h0.x, a.h0.y, a.h0.z, a.h0.w, a.h1.x, a.h1.y, a.h1.z, a.h1.w};
+  const uint32_t al[8] = {a.l0.x, a.l0.y, a.l0.z, a.l0.w, a.l1.x, a.l1.y, a.l1.z, a.l1.w};
   const uint32_t bh[8] = {b.h0.x, b.h0.y, b.h0.z, b.h0.w, b.h1.x, b.h1.y, b.h1.z, b.h1.w};
-  const uint32_t ar[4] = {a.r.x, a.r.y, a.r.z, a.r.w}, br[4] = {b.r.x, b.r.y, b.r.z, b.r.w};
+  const uint32_t bl[8] = {b.l0.x, b.l0.y, b.l0.z, b.l0.w, b.l1.x, b.l1.y, b.l1.z, b.l1.w};
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const uint16_t ha = (uint16_t)(ah[e >> 1] >> (16 * (e & 1))), hb = (uint16_t)(bh[e >> 1] >> (16 * (e & 1)));
-    const int8_t ra = (int8_t)(ar[e >> 2] >> (8 * (e & 3))), rb = (int8_t)(br[e >> 2] >> (8 * (e & 3)));
-    acc = fma((double)r8_value(ha, ra), (double)r8_value(hb, rb), acc);
-  }
+  for (int e = 0; e < 16; ++e)
+    acc = fma(l16_x(ah[e >> 1], al[e >> 1], e & 1), l16_x(bh[e >> 1], bl[e >> 1], e & 1), acc);
   return acc;
 }
 // the wave's level-2 scores of P pairs (rows qr[p] of the query planes, gc[p] of the gallery planes), every
 // load of all P pairs in flight before the sums; d_pad % 64 == 0 (a lane's 16 elements are all in or all out)
 template <int P>
-__device__ __forceinline__ void r8_scores(const SimArgs& a, const int64_t (&qr)[P], const int64_t (&gc)[P], int lane,
+__device__ __forceinline__ void l16_scores(const SimArgs& a, const int64_t (&qr)[P], const int64_t (&gc)[P], int lane,
                                           double (&s2)[P]) {
 #pragma unroll
   for (int p = 0; p < P; ++p) s2[p] = 0.0;
   for (int64_t k0 = 0; k0 < a.ldk; k0 += 1024) {
     const int64_t k = k0 + 16 * lane;
     if (k < a.ldk) {
-      R8Frag fq[P], fg[P];
+      L16Frag fq[P], fg[P];
 #pragma unroll
       for (int p = 0; p < P; ++p) {
-        r8_load(a.qhi + qr[p] * a.ldk, a.q_r8 + qr[p] * a.ldk, k, fq[p]);
-        r8_load(a.ghi + gc[p] * a.ldk, a.g_r8 + gc[p] * a.ldk, k, fg[p]);
+        l16_load(a.qhi + qr[p] * a.ldk, a.q_lo16 + qr[p] * a.ldk, k, fq[p]);
+        l16_load(a.ghi + gc[p] * a.ldk, a.g_lo16 + gc[p] * a.ldk, k, fg[p]);
       }
 #pragma unroll
-      for (int p = 0; p < P; ++p) s2[p] = r8_partial(fq[p], fg[p], s2[p]);
+      for (int p = 0; p < P; ++p) s2[p] = l16_partial(fq[p], fg[p], s2[p]);
     }
   }
 #pragma unroll
@@ -287,6 +297,13 @@ constexpr size_t stage_bytes() {
   return (size_t)((MODE == CMVE_SIM_BF16X3 && !PHASED) ? 2 : 1) * (BM + BN) * BK * 2;
 }
 
+// the ring loop's geometries (G64, 128 x 64 and the 8-wave 128 x 128 of the batches); the others take the 2-stage
+// loop (G128) or the phased G256 schedule
+template <int BM, int BN, bool PHASED, int NW = 4>
+constexpr bool is_ring() {
+  return !PHASED && (BN == 64 || (BM == 128 && BN == 128 && NW == 8)) && (BM == 64 || BM == 128);
+}
+
 // staging ring depth of the 2-stage (non-phased) loop: the G64 tiles of small problems keep NS - 1
 // K-tiles in flight (a 1k x 1k x 1024 GEMM is latency-bound: with 2 stages every one of its 16 K-tiles
 // exposed a full L2 / Infinity-Cache round trip, ~1.2 us each against ~0.1 us of MFMAs).  4 stages
@@ -369,13 +386,17 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_BATCH_FIX1
 #define CMVE_BATCH_FIX1 1
 #endif
-#ifndef CMVE_R8_P
-#define CMVE_R8_P 2  // K14 level-2 re-score: pairs per wave in flight at once
+#ifndef CMVE_L2_P
+#define CMVE_L2_P 1  // K14 level-2 re-score: pairs per wave in flight at once (2: 128+ VGPRs, spills at 4 waves per SIMD)
 #endif
 // BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): the block picks the problem's
 // argument block in `tab` (see batch_item below); otherwise `tab` is unused
+#ifndef CMVE_BATCH_WPE
+#define CMVE_BATCH_WPE 4  // the batch ring kernels: waves per SIMD the register budget must allow (<= 128 VGPRs)
+#endif
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
-__global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2) void sim_kernel(
+__global__ __launch_bounds__(WM * WN * 64, BATCH ? CMVE_BATCH_WPE : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2))
+void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
   // a batch's blocks: the (evaluation, tile) pairs in evaluation-major order, cut into 8 contiguous ranges, one per
   // XCD -- an XCD works through one or two evaluations at a time (a 1k-A evaluation's fp16 planes are 4 MB, its
@@ -420,7 +441,8 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
 #endif
 
   // the G64 ring rank kernel re-scores its undecided pairs itself when the K14 host asks (SimArgs::fix_inline)
-  constexpr bool INL = EPI == EPI_RANK && NS > 2;
+  constexpr bool RING = is_ring<BM, BN, PHASED, NW>();
+  constexpr bool INL = EPI == EPI_RANK && RING;
   __shared__ EpiLds<BM, BN, epi_thr(EPI), INL> epi;
   double sgt_pub = 0.0;  // INL: this thread's row / column GT score (tid < BM + BN), published with the thresholds
   int* lds_rc = epi.rc;
@@ -532,10 +554,10 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) gt_row[i][r] = a.row_gt1[rb + i * 16 + r];  // (n_pad entries)
+          for (int r = 0; r < 4; ++r) gt_row[i][r] = gld(a.row_gt1 + rb + i * 16 + r);  // (n_pad entries)
       if (a.col_gt1)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) gt_col[j] = a.col_gt1[cb + j * 16];
+        for (int j = 0; j < TN; ++j) gt_col[j] = gld(a.col_gt1 + cb + j * 16);
     }
   };
 
@@ -828,7 +850,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
       bool inl = false;  // inline fix-up: the pair total is added after the flush (a returning atomic here stayed
                          // in vmcnt, so the re-score's first load wait also waited for its round trip)
       if constexpr (INL) inl = a.fix_inline != 0;
-      if (total && lane == 0 && !inl) wbase = atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);
+      if (total && lane == 0 && !inl) wbase = gadd(a.bucket_cnt + bucket, (unsigned long long)total);
       if constexpr (INL) {
         if (a.fix_inline) {
           // fp64 re-score of the tile's undecided pairs (fixup_walk's arithmetic: the same scores), counted
@@ -866,11 +888,13 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
 #endif
           if (listed) {
             CMVE_BAR_LDS();
-            if (a.q_r8) {
-              // level 2: each wave scores CMVE_R8_P listed pairs at once from the fp16 + r8 planes (r8_scores) and
-              // decides every direction whose GT score lies outside s2 +- E2; the directions left undecided stay in
-              // the entry's flags for the fp64 pass below (the wave owns its entries: no other wave touches them)
-              constexpr int RP = CMVE_R8_P;
+            if (a.q_lo16) {
+              // level 2: each wave scores CMVE_L2_P listed pairs at once from the fp16 + bf16 residual planes
+              // (l16_scores) and decides every direction whose GT score lies outside s2 +- E2; a pair with a
+              // direction left undecided goes to the level-3 list (fp64 in the finish launch, off this kernel's
+              // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
+              // entries: no other wave touches them)
+              constexpr int RP = CMVE_L2_P;
               for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
                 int64_t qr[RP], gc[RP];
                 uint32_t ent[RP];
@@ -881,12 +905,12 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                   gc[u] = n0 + ((ent[u] >> 8) & 0xff);
                 }
                 double s2[RP];
-                r8_scores<RP>(a, qr, gc, lane, s2);
+                l16_scores<RP>(a, qr, gc, lane, s2);
                 if (lane == 0) {
 #pragma unroll
                   for (int u = 0; u < RP; ++u) {
                     if (p0 + u >= ntot) break;
-                    const double eq = (double)a.q_e8[qr[u]], eg = (double)a.g_e8[gc[u]];
+                    const double eq = (double)gld(a.q_el + qr[u]), eg = (double)gld(a.g_el + gc[u]);
                     const double E2 = eq + (1.0 + eq) * eg + 2e-12;
                     uint32_t fl = (ent[u] >> 16) & 3u;
                     const int lr = (int)(ent[u] & 0xff), lc = (int)((ent[u] >> 8) & 0xff);
@@ -900,6 +924,14 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                       if (s2[u] - E2 > t) { lds_add_u32_async(&lds_cc[lc], 1); fl &= ~2u; }
                       else if (s2[u] + E2 < t) fl &= ~2u;
                     }
+                    if (fl && a.l3) {  // level 3 in the finish (a returning atomic: only these few pairs pay it)
+                      const unsigned slot = gadd(a.l3_count, 1u);
+                      if (slot < (unsigned)a.l3_cap) {
+                        gst(a.l3 + slot, (unsigned long long)qr[u] | ((unsigned long long)gc[u] << 31) |
+                                             ((unsigned long long)fl << 62));
+                        fl = 0u;
+                      }
+                    }
                     epi.list[p0 + u] = (ent[u] & 0xffffu) | (fl << 16);
                   }
                 }
@@ -910,7 +942,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
               const int64_t r1 = m0 + (e1 & 0xff), c1 = n0 + ((e1 >> 8) & 0xff);
               const int64_t r2 = two ? m0 + (e2 & 0xff) : r1, c2 = two ? n0 + ((e2 >> 8) & 0xff) : c1;
               // the norms travel with the rows (loaded after the dot they were a second round trip)
-              const double inv1 = a.q_inv[r1] * a.g_inv[c1], inv2 = a.q_inv[r2] * a.g_inv[c2];
+              const double inv1 = gld(a.q_inv + r1) * gld(a.g_inv + c1), inv2 = gld(a.q_inv + r2) * gld(a.g_inv + c2);
               double d1, d2;
               if (a.q_f64) {
                 const double* q = (const double*)a.q_raw;
@@ -950,7 +982,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                 const uint32_t e = epi.list[p];
                 if (!(e >> 16)) continue;  // decided at level 2
                 const int64_t r1 = m0 + (e & 0xff), c1 = n0 + ((e >> 8) & 0xff);
-                const double inva = a.q_inv[r1], invb = a.g_inv[c1];
+                const double inva = gld(a.q_inv + r1), invb = gld(a.g_inv + c1);
                 double s1;
                 if (a.q_f64) {
                   const double* x = (const double*)a.q_raw + r1 * a.q_ld;
@@ -966,7 +998,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                   if ((e >> 17) & 1u) { if (s1 > epi.sgt[BM + c1 - n0]) lds_add_u32_async(&lds_cc[c1 - n0], 1); }
                 }
               }
-            } else if (a.q_r8) {  // level 3 after level 2: the few pairs left, one at a time per wave
+            } else if (a.q_lo16) {  // level 3 after level 2 (a full level-3 list): one pair at a time per wave
               for (int p = wave; p < ntot; p += NW) {
                 const uint32_t e = epi.list[p];
                 if (e >> 16) rescore2(e, 0u, false);
@@ -990,7 +1022,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
                 const int lr = wr * (TM * 16) + (src >> 4) * 4 + i * 16 + (bit & 3);
                 const int lc = wc * (TN * 16) + (src & 15) + (bit >> 2) * 16;
                 const int64_t row = m0 + lr, col = n0 + lc;
-                const double inva = a.q_inv[row], invb = a.g_inv[col];
+                const double inva = gld(a.q_inv + row), invb = gld(a.g_inv + col);
                 double sc;
                 if (a.q_f64) {
                   const double* x = (const double*)a.q_raw + row * a.q_ld;
@@ -1021,12 +1053,12 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
         lds_rc[t] = 0;  // owner thread: ready for the next tile
         if (!c) continue;
         if (t < BM) {
-          if (a.row_cnt && m0 + t < a.nq) atomicAdd(&a.row_cnt[m0 + t], c);
+          if (a.row_cnt && m0 + t < a.nq) gadd(a.row_cnt + m0 + t, c);
         } else {
-          if (a.col_cnt && n0 + t - BM < a.ng) atomicAdd(&a.col_cnt[n0 + t - BM], c);
+          if (a.col_cnt && n0 + t - BM < a.ng) gadd(a.col_cnt + n0 + t - BM, c);
         }
       }
-      if (inl && total && lane == 0) atomicAdd(a.bucket_cnt + bucket, (unsigned long long)total);  // (no return)
+      if (inl && total && lane == 0) gadd(a.bucket_cnt + bucket, (unsigned long long)total);  // (no return)
       const bool emit = total != 0u && !inl;  // (inline: re-scored above; the bucket count is the pair total)
       if (emit) {
         unsigned long long slot = __shfl(wbase, 0, 64) + excl;
@@ -1053,7 +1085,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
               packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
                        ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
             }
-            if ((long long)slot < a.cap_b) dst[slot] = packed;
+            if ((long long)slot < a.cap_b) gst(dst + slot, packed);
             ++slot;
           }
         }
@@ -1237,7 +1269,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
 #undef CMVE_BAR
-  } else if constexpr (NS > 2) {
+  } else if constexpr (RING) {
   // ---- ring of NS stages (G64): K-tiles t+1 .. t+NS-2 stay in flight while K-tile t is consumed ----
   constexpr int LPS = (BM / 8 / NW + BN / 8 / NW) * (MODE == CMVE_SIM_BF16X3 ? 2 : 1);  // loads / stage / wave
   static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
@@ -1249,8 +1281,8 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
   unsigned emq = 0u, emg = 0u;
   if constexpr (epi_thr(EPI)) {
     if (a.thr_gt) {
-      emq = a.q_emax[lane];
-      emg = a.g_emax[lane];
+      emq = gld(a.q_emax + lane);
+      emg = gld(a.g_emax + lane);
     }
   }
   for (int t = 0; t < NS - 1 && t < nk0; ++t) stage(t, t);
@@ -1262,8 +1294,8 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * TM * 16 == 64 && WN == 1) ? CMV
   if constexpr (epi_thr(EPI)) {
     if (a.thr_gt) {
       if (thr_dir) {
-        sgt_raw = tid < BM ? a.row_sgt[m0 + tid] : a.col_sgt[n0 + tid - BM];
-        e_raw = tid < BM ? a.q_err[m0 + tid] : a.g_err[n0 + tid - BM];
+        sgt_raw = tid < BM ? gld(a.row_sgt + m0 + tid) : gld(a.col_sgt + n0 + tid - BM);
+        e_raw = tid < BM ? gld(a.q_err + m0 + tid) : gld(a.g_err + n0 + tid - BM);
       }
       fetch_gt1();
     }
@@ -1818,9 +1850,12 @@ extern "C" int cmve_linear(cmve_handle_t h, const cmve_rows_t* x, const cmve_row
 
 namespace {
 struct EvalWs {
-  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, q_gt1, g_gt1, q_e8, g_e8, q_r8, g_r8, cand, total;
+  size_t done, q_sgt, q_hi, q_lo, q_cnt, g_sgt, g_hi, g_lo, g_cnt, q_gt1, g_gt1, q_el, g_el, q_l16, g_l16, l3, cand,
+      total;
 };
-// (the r8 planes: [n_pad, d_pad] int8 each side, the level-2 re-score's residuals; r8_elem)
+// the lo16 planes: [n_pad, d_pad] bf16 each side, the level-2 re-score's residuals (lo16_elem); l3: the level-3
+// list (a count word, then EVAL_L3_CAP entries)
+constexpr int EVAL_L3_CAP = 4096;
 EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t d_pad, int64_t cand_cap) {
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   EvalWs w;
@@ -1847,14 +1882,16 @@ EvalWs eval_ws_layout(int64_t nq_pad, int64_t ng_pad, int64_t d_pad, int64_t can
   o = up(o + 4 * (size_t)nq_pad);
   w.g_gt1 = o;
   o = up(o + 4 * (size_t)ng_pad);
-  w.q_e8 = o;
+  w.q_el = o;
   o = up(o + 4 * (size_t)nq_pad);
-  w.g_e8 = o;
+  w.g_el = o;
   o = up(o + 4 * (size_t)ng_pad);
-  w.q_r8 = o;
-  o = up(o + (size_t)nq_pad * (size_t)d_pad);
-  w.g_r8 = o;
-  o = up(o + (size_t)ng_pad * (size_t)d_pad);
+  w.q_l16 = o;
+  o = up(o + 2 * (size_t)nq_pad * (size_t)d_pad);
+  w.g_l16 = o;
+  o = up(o + 2 * (size_t)ng_pad * (size_t)d_pad);
+  w.l3 = o;
+  o = up(o + 8 + 8 * (size_t)EVAL_L3_CAP);
   w.cand = o;
   o = up(o + 8 * (size_t)cand_cap);
   w.total = o;
@@ -2055,21 +2092,28 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   const char* fix_env = getenv("CMVE_EVAL_FIX_LAUNCH");  // kernel studies / tests: the separate fix-up launch
   const bool no_inline = fix_env && atoi(fix_env) != 0;
   P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
-  // level-2 re-score from the fp16 + r8 planes: the F16 mode whose prep runs the register path (the only one
-  // that writes r8: 16-B row pieces, d_pad <= 1024, both sides); CMVE_EVAL_NO_R8 (tests / kernel studies) off
-  static const bool no_r8 = [] {
-    const char* e = getenv("CMVE_EVAL_NO_R8");
+  // level-2 re-score from the fp16 + bf16 residual planes: the F16 mode whose prep runs the register path (the
+  // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides); level 3 deferred to the finish through
+  // the workspace's list.  CMVE_EVAL_NO_L2 (tests / kernel studies): every band pair in fp64 in the GEMM
+  static const bool no_l2 = [] {
+    const char* e = getenv("CMVE_EVAL_NO_L2");
     return e && atoi(e) != 0;
   }();
-  if (P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_r8) {
-    P.sq.r8 = (int8_t*)(base + w.q_r8);
-    P.sg.r8 = (int8_t*)(base + w.g_r8);
-    P.sq.err_r8 = (float*)(base + w.q_e8);
-    P.sg.err_r8 = (float*)(base + w.g_e8);
-    a.q_r8 = P.sq.r8;
-    a.g_r8 = P.sg.r8;
-    a.q_e8 = P.sq.err_r8;
-    a.g_e8 = P.sg.err_r8;
+  if (P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2) {
+    P.sq.lo16 = (uint16_t*)(base + w.q_l16);
+    P.sg.lo16 = (uint16_t*)(base + w.g_l16);
+    P.sq.err_lo16 = (float*)(base + w.q_el);
+    P.sg.err_lo16 = (float*)(base + w.g_el);
+    a.q_lo16 = P.sq.lo16;
+    a.g_lo16 = P.sg.lo16;
+    a.q_el = P.sq.err_lo16;
+    a.g_el = P.sg.err_lo16;
+    c.l3_count = (unsigned*)(base + w.l3);
+    c.l3 = (uint64_t*)(base + w.l3 + 8);
+    c.l3_cap = EVAL_L3_CAP;
+    a.l3_count = c.l3_count;
+    a.l3 = (unsigned long long*)c.l3;
+    a.l3_cap = c.l3_cap;
   }
   if (P.inline_fix) {
     a.fix_inline = 1;
@@ -2155,6 +2199,7 @@ struct cmve_eval_batch {
   int64_t nq_pad = 0, ng_pad = 0;
   int bm = 64, bn = 64;           // the rank tile (batch_geo_bm / _bn)
   cmve::EvalSide sq0, sg0;        // the shapes (the launch grids)
+  cmve::EvalCommon c0;            // (the first evaluation's: which prep kernel applies)
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
 };
@@ -2255,6 +2300,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->bn = batch_geo_bn(b->nq_pad, b->ng_pad, b->mode);
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;
+  b->c0 = P0.c;
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
   if (e == hipSuccess) e = hipMalloc(&b->d_args, sizeof(SimArgs) * (size_t)count);
   if (e == hipSuccess)
@@ -2292,7 +2338,7 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   hipStream_t s = h->stream;
   if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
   arm(0);
-  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
+  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
   arm(1);
@@ -2304,7 +2350,7 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
   arm(3);
-  st = cmve::launch_eval_batch(b->sq0, b->sg0, b->d_items, b->count, b->qf, b->gf, 2, s);
+  st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
   return CMVE_OK;

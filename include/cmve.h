@@ -390,19 +390,22 @@ int cmve_gt_ranks(cmve_handle_t h, const int32_t* cnt, const double* sgt, int64_
  * ws: cmve_eval_workspace bytes, ZEROED ONCE when allocated (its err_max shards reset themselves).
  * out (int64, 16 + q->n + g->n): out[0..4) t2v #rank<=1, #<=5, #<=10, sum of ranks; out[4..8) the same
  * for v2t; out[8] undecided pairs; out[9] 0, or the cand_cap a retry needs (a bucket overflowed: the
- * ranks are incomplete); out[16 ..] t2v ranks, then v2t ranks (1-based; cmve_gt_ranks' rules).
+ * ranks are incomplete); out[11] captions failing the CMVE_EVAL_PAIRED check; out[12] level-3 pairs; out[16 ..] t2v ranks, then v2t ranks (1-based; cmve_gt_ranks' rules).
  * timing_slot in [0, CMVE_EVAL_TIMING_SLOTS) records handle events around the launches
  * (cmve_eval_timing reads them) and each launch's own start / stop (cmve_eval_kernel_timing); -1 records none.
  * mode may carry CMVE_EVAL_PAIRED: the caller asserts a one-to-one GT pairing -- every t2v list is one
  * video p = row_idx[row_off[i]], every v2t list is one caption, and v2t(p) = [i] (MSR-VTT-1kA's
  * structure; q->n == g->n) -- and launch 1 then packs and scores each (caption, video) pair in one wave
- * (half the row reads; same results bit for bit).  Launch 1 checks the assertion per caption (t2v(i) = [p],
- * 0 <= p < g->n, v2t(p) = [i]); a caption that fails it writes nothing of side g, ranks as if its list
- * were empty and is counted in out[11] (0 for a true pairing): with out[11] != 0 the ranks are undefined,
- * but no write leaves the workspace / planes and no row is written by two waves.
- * At F16 size with d_pad <= 1024 and 16-B aligned rows the workspace also holds an 8-bit residual plane of
- * each side (x_hat - fp16 plane, in 1/256 ulps of the fp16 element): launch 2 decides a band pair from
- * fp16 + residual (error <= e8_q + (1 + e8_q) e8_g, ~2e-6) and re-scores in fp64 only the pairs within that.
+ * (half the row reads; same results bit for bit).  Launch 1 checks the t2v side of the assertion per
+ * caption (one GT, 0 <= p < g->n); a caption that fails it writes nothing of side g, ranks as if its list
+ * were empty and is counted in out[11] (0 for a valid pairing): with out[11] != 0 the ranks are undefined,
+ * but no write leaves the workspace / planes.  Lists whose v2t side is not the inverse (two captions naming
+ * one video) give undefined ranks: both waves write that video's row (within bounds).
+ * At F16 size with d_pad <= 1024 and 16-B aligned rows the workspace also holds a bf16 residual plane of
+ * each side (x_hat - fp16 plane): launch 2 decides a band pair from fp16 + residual (error <= el_q +
+ * (1 + el_q) el_g, ~7e-7) and lists the pairs within that bound (out[12] counts them; ~4 per 1k-A
+ * evaluation), which the last launch re-scores in fp64 before it ranks (a full list: launch 2 re-scores the
+ * rest itself).
  */
 #define CMVE_EVAL_TIMING_SLOTS 32
 #define CMVE_EVAL_PAIRED 0x100

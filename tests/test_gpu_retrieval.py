@@ -904,3 +904,39 @@ def test_rank_batch_dense_tiles(torch_cuda, case):
         assert h[9] == 0 and h[8] > 4 * 1024  # no overflow; the dense tiles went past the LDS list
         assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True])
+def test_level3_list_overflow(torch_cuda, batched):
+    """The rank GEMM's level-3 list (pairs its level-2 re-score leaves undecided, re-scored in fp64 by the finish
+    launch) past its 4,096 entries: 125 groups of 8 near-duplicate captions / videos (3e-4 noise: every pair inside
+    a group is within the level-2 bound, yet no pair of scores is closer than 1e-12) put ~7,000 such pairs in
+    listed tiles (<= 1,024 band pairs each); the entries past the list are re-scored inside the GEMM.  Ranks ==
+    the oracle's exact counts in both directions, single evaluation and batch; out[12] reports the level-3 count."""
+    import torch
+    from cmve import engine
+    rng = np.random.default_rng(5)
+    n, d, gsz = 1000, 256, 8
+    base = rng.standard_normal((n // gsz + 1, d))
+    gi = np.arange(n) // gsz
+    v = base[gi] + 3e-4 * rng.standard_normal((n, d))
+    c = base[gi] + 3e-4 * rng.standard_normal((n, d))
+    ids = [[i] for i in range(n)]
+    s = R.exact_scores64(c, v)
+    er, ec = R.rank_counts(s, ids), R.rank_counts(s.T, ids)
+    ct, vt = torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda()
+    if batched:
+        sess = [engine.RankSession(n, n, d, row_gts=ids, col_gts=ids, dtype=torch.float64) for _ in range(2)]
+        b = engine.RankBatch(sess, [(ct, vt), (ct.clone(), vt.clone())])
+        b.run()
+        torch.cuda.synchronize()
+        outs = [x.out.cpu().numpy() for x in sess]
+        b.close()
+    else:
+        sess = engine.RankSession(n, n, d, row_gts=ids, col_gts=ids, dtype=torch.float64)
+        sess.run(ct, vt)
+        outs = [sess.out.cpu().numpy()]
+    for h in outs:
+        assert h[9] == 0 and h[12] > 4096, (h[8], h[12])
+        assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)

@@ -26,17 +26,22 @@ ROLES = ("pack_gt_scores", "rank_gemm", "fixup", "ranks_recall")
 
 
 def role(name):
-    # (single evaluations and batches: eval_*_batch_kernel, sim_kernel<..., true>; one profile holds one form)
+    """The evaluation launch a kernel name is; the batch kernels (cmve_eval_batch_*: the headline's timed loop)
+    and the single-evaluation kernels (cmve_eval_ranks: the bench's latency measurements) are kept apart, so a
+    profile holding both never averages one into the other."""
+    batch = "_batch_kernel" in name or ("sim_kernel<2, 1" in name and ", true>" in name)
     if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name or "eval_prep_pair_batch_kernel" in name \
             or "eval_prep_batch_kernel" in name:
-        return "pack_gt_scores"
-    if "eval_fix_kernel" in name:
-        return "fixup"
-    if "eval_finish_kernel" in name or "eval_finish_batch_kernel" in name:
-        return "ranks_recall"
-    if "sim_kernel<2, 1" in name:
-        return "rank_gemm"
-    return None
+        r = "pack_gt_scores"
+    elif "eval_fix_kernel" in name:
+        r = "fixup"
+    elif "eval_finish_kernel" in name or "eval_finish_batch_kernel" in name:
+        r = "ranks_recall"
+    elif "sim_kernel<2, 1" in name:
+        r = "rank_gemm"
+    else:
+        return None
+    return r if batch else r + "_single"
 
 
 def main(outdir, tag):
@@ -51,6 +56,17 @@ def main(outdir, tag):
             k = role(r.get("Kernel_Name", ""))
             if k and r.get("Counter_Name") == counter:
                 per[k][counter].append(float(r["Counter_Value"]))
+    # the counter passes are kernel traces of the same command too: their per-launch durations beside the trace's
+    pdur = defaultdict(list)
+    for r in rows(os.path.join(outdir, "fetch", "**", "*counter_collection.csv")):
+        k = role(r.get("Kernel_Name", ""))
+        if k and r.get("Counter_Name") == "FETCH_SIZE":
+            pdur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+    sq = defaultdict(lambda: defaultdict(list))
+    for r in rows(os.path.join(outdir, "sq", "**", "*counter_collection.csv")):
+        k = role(r.get("Kernel_Name", ""))
+        if k:
+            sq[k][r.get("Counter_Name")].append(float(r["Counter_Value"]))
     dur, evals = defaultdict(list), defaultdict(list)
     for r in rows(os.path.join(outdir, "trace", "**", "*kernel_trace.csv")):
         k = role(r.get("Kernel_Name", ""))
@@ -58,7 +74,9 @@ def main(outdir, tag):
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
             evals[k].append(int(r.get("Grid_Size_Y") or 1))  # batches: grid y = the evaluations
     kernels = {}
-    for k in ROLES:
+    batch_mode = any(len(dur[k]) for k in ROLES)
+    roles = ROLES if batch_mode else tuple(k + "_single" for k in ROLES)
+    for k in ROLES + tuple(k + "_single" for k in ROLES):
         f, w = per[k]["FETCH_SIZE"], per[k]["WRITE_SIZE"]
         e = {"launches_traced": len(dur[k]),
              "evaluations_per_launch": (max(set(evals[k]), key=evals[k].count)) if evals[k] else None,
@@ -66,10 +84,19 @@ def main(outdir, tag):
              "trace_total_ms": sum(dur[k]),
              "fetch_kib_per_launch": (sum(f) / len(f)) if f else None,
              "write_kib_per_launch": (sum(w) / len(w)) if w else None}
+        if dur[k]:
+            e["trace_median_ms"] = sorted(dur[k])[len(dur[k]) // 2]
+        if pdur[k]:
+            e["fetch_pass_avg_ms"] = sum(pdur[k]) / len(pdur[k])
         if f and w:
             e["hbm_bytes_per_launch"] = 2 * e["fetch_kib_per_launch"] * 1024 + e["write_kib_per_launch"] * 1024
+        if sq[k]:
+            med = {c: sorted(v)[len(v) // 2] for c, v in sq[k].items()}
+            e["sq_per_launch_median"] = med
+            if med.get("SQ_WAVES"):
+                e["valu_insts_per_wave"] = med.get("SQ_INSTS_VALU", 0) / med["SQ_WAVES"]
         kernels[k] = e
-    dominant = max(ROLES, key=lambda k: kernels[k]["trace_total_ms"])
+    dominant = max(roles, key=lambda k: kernels[k]["trace_total_ms"])
     out = {"tag": tag, "workload": "MSR-VTT-1kA exact evaluation, 1000 x 1000 x 1024, float64 inputs",
            "kernels": kernels, "dominant": dominant,
            "hbm_bytes_per_launch": kernels[dominant].get("hbm_bytes_per_launch"),
