@@ -429,6 +429,51 @@ __device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double 
   return wave_dot64(xa, xb, d, lane) * (inva * invb);
 }
 
+// ---- K14 level-2 re-score: one pair's score from the fp16 + bf16 residual planes (lo16_elem, cmve_internal.h) ----
+// lane L holds elements [16L, 16L + 16) of each 1024-element chunk: two 16-B fp16 loads and two 16-B bf16 loads
+// per row and chunk.  x2 = h + lo is formed in fp64 (exact unless lo lies 2^-42 below h: then within 2^-53 |x2|),
+// the products and sums in fp64, so the sum's error is a few ulps of 1:
+//   |s2 - cos64| <= el_q + (1 + el_q) el_g + 2e-12
+// (the 2e-12 covers the fp64 sums here and in cos64, as score_error_bound's 1e-12 does for the MFMA bound)
+typedef uint32_t cmve_u32x4 __attribute__((ext_vector_type(4)));
+struct L16Frag {
+  cmve_u32x4 h0, h1, l0, l1;
+};
+__device__ __forceinline__ void l16_load(const uint16_t* __restrict__ hrow, const uint16_t* __restrict__ lrow,
+                                         int64_t k, L16Frag& f) {
+  f.h0 = gld((const cmve_u32x4*)(hrow + k));
+  f.h1 = gld((const cmve_u32x4*)(hrow + k + 8));
+  f.l0 = gld((const cmve_u32x4*)(lrow + k));
+  f.l1 = gld((const cmve_u32x4*)(lrow + k + 8));
+}
+__device__ __forceinline__ double l16_x(uint32_t hw, uint32_t lw, int half) {
+  const uint16_t h = (uint16_t)(hw >> (16 * half));
+  const uint32_t l = half ? (lw & 0xffff0000u) : (lw << 16);
+  return (double)(float)__builtin_bit_cast(_Float16, h) + (double)__uint_as_float(l);
+}
+__device__ __forceinline__ double l16_partial(const L16Frag& a, const L16Frag& b, double acc) {
+  const uint32_t ah[8] = {a.h0.x, a.h0.y, a.h0.z, a.h0.w, a.h1.x, a.h1.y, a.h1.z, a.h1.w};
+  const uint32_t al[8] = {a.l0.x, a.l0.y, a.l0.z, a.l0.w, a.l1.x, a.l1.y, a.l1.z, a.l1.w};
+  const uint32_t bh[8] = {b.h0.x, b.h0.y, b.h0.z, b.h0.w, b.h1.x, b.h1.y, b.h1.z, b.h1.w};
+  const uint32_t bl[8] = {b.l0.x, b.l0.y, b.l0.z, b.l0.w, b.l1.x, b.l1.y, b.l1.z, b.l1.w};
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    acc = fma(l16_x(ah[e >> 1], al[e >> 1], e & 1), l16_x(bh[e >> 1], bl[e >> 1], e & 1), acc);
+  return acc;
+}
+// one pair's level-2 score (every lane gets the same bits): rows of the fp16 and bf16 residual planes, d_pad % 64 == 0
+__device__ __forceinline__ double l16_score1(const uint16_t* hq, const uint16_t* lq, const uint16_t* hg,
+                                             const uint16_t* lg, int64_t d_pad, int lane) {
+  double acc = 0.0;
+  for (int64_t k = 16 * (int64_t)lane; k < d_pad; k += 1024) {
+    L16Frag a, b;
+    l16_load(hq, lq, k, a);
+    l16_load(hg, lg, k, b);
+    acc = l16_partial(a, b, acc);
+  }
+  return wave_sum(acc);
+}
+
 // XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
 // x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
 // on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
@@ -436,6 +481,59 @@ __device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double 
 // bandwidth-bound bench-size fix-up that was 3% slower)
 // flat: one group over all buckets and every wave of the grid (small evaluations: a 1k-row gallery has
 // 4 buckets, which the XCD grouping would leave to 4 of the 8 XCDs); the caller keeps nb <= 4096
+// the level-2 planes of an evaluation's fix-up (K14 with the bf16 residual planes): h16 / lo16 of both sets, their
+// per-row bounds and the plane stride; qh == nullptr: every pair in fp64
+struct L2Planes {
+  const uint16_t* qh = nullptr;
+  const uint16_t* ql = nullptr;
+  const uint16_t* gh = nullptr;
+  const uint16_t* gl = nullptr;
+  const float* qe = nullptr;
+  const float* ge = nullptr;
+  int64_t ldk = 0;
+};
+
+// the exclusive prefix of the bucket sizes a fix-up walks (wave 0 of the block): buckets xcd, xcd + G, ..., nk
+// of them, each clamped to cap_b; pre[nk] = the total (lane-chunked sums + a wave scan)
+__device__ __forceinline__ void fixup_prefix(const uint64_t* __restrict__ cand, int64_t nb, int64_t cap_b, int xcd,
+                                             int G, int64_t nk, int lane, int64_t* pre) {
+  const int64_t per = (nk + 63) / 64;
+  const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
+  if (per <= 4) {  // (<= 256 buckets: one round of loads held in registers)
+    int64_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (k0 + j < k1) ? min((int64_t)gld(cand + xcd + G * (k0 + j)), cap_b) : 0;
+    const int64_t sum = (v[0] + v[1]) + (v[2] + v[3]);
+    int64_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int64_t run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k0 + j < k1) {
+        pre[k0 + j] = run;
+        run += v[j];
+      }
+    if (lane == 63) pre[nk] = incl;
+  } else {
+    int64_t sum = 0;
+    for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)gld(cand + xcd + G * k), cap_b);
+    int64_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    int64_t run = incl - sum;
+    for (int64_t k = k0; k < k1; ++k) {
+      pre[k] = run;
+      run += min((int64_t)gld(cand + xcd + G * k), cap_b);
+    }
+    if (lane == 63) pre[nk] = incl;
+  }
+}
+
 template <typename TQ, typename TG, bool PREFETCH = false>
 __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -443,49 +541,14 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t nb, int64_t cap_b, bool flat = false) {
+                                                    int64_t nb, int64_t cap_b, bool flat = false,
+                                                    const L2Planes l2 = L2Planes{}) {
   __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = flat ? 1 : 8;  // bucket groups (XCDs)
   const int xcd = flat ? 0 : (blockIdx.x & 7);
   const int64_t nk = xcd < nb ? (nb - xcd + G - 1) / G : 0;
-  if (wave == 0) {  // prefix of this XCD's bucket sizes: lane-chunked sums + a wave scan
-    const int64_t per = (nk + 63) / 64;
-    const int64_t k0 = lane * per, k1 = min(nk, k0 + per);
-    if (per <= 4) {  // (<= 256 buckets: one round of loads held in registers)
-      int64_t v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (k0 + j < k1) ? min((int64_t)cand[xcd + G * (k0 + j)], cap_b) : 0;
-      const int64_t sum = (v[0] + v[1]) + (v[2] + v[3]);
-      int64_t incl = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      int64_t run = incl - sum;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (k0 + j < k1) {
-          pre[k0 + j] = run;
-          run += v[j];
-        }
-      if (lane == 63) pre[nk] = incl;
-    } else {
-      int64_t sum = 0;
-      for (int64_t k = k0; k < k1; ++k) sum += min((int64_t)cand[xcd + G * k], cap_b);
-      int64_t incl = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      int64_t run = incl - sum;
-      for (int64_t k = k0; k < k1; ++k) {
-        pre[k] = run;
-        run += min((int64_t)cand[xcd + G * k], cap_b);
-      }
-      if (lane == 63) pre[nk] = incl;
-    }
-  }
+  if (wave == 0) fixup_prefix(cand, nb, cap_b, xcd, G, nk, lane, pre);
   __syncthreads();
   const int64_t total = pre[nk];
   const int nw = (int)(blockDim.x >> 6);  // waves per block
@@ -501,19 +564,42 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
       }
       k = lo;
     }
-    const uint64_t u = cand[nb + (xcd + G * k) * cap_b + (c - pre[k])];
+    const uint64_t u = gld(cand + nb + (xcd + G * k) * cap_b + (c - pre[k]));
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
-    const uint32_t flags = (uint32_t)(u >> 62);
+    uint32_t flags = (uint32_t)(u >> 62);
+    if (l2.qh && flags) {
+      // level 2: the pair from the fp16 + bf16 residual planes (one round trip of 8 KiB, the planes the rank GEMM
+      // just read); a direction whose GT score lies outside s2 +- E2 is decided here, the rest in fp64 below
+      const double s2 = l16_score1(l2.qh + i * l2.ldk, l2.ql + i * l2.ldk, l2.gh + j * l2.ldk, l2.gl + j * l2.ldk,
+                                   l2.ldk, lane);
+      const double eq = (double)gld(l2.qe + i), eg = (double)gld(l2.ge + j);
+      const double E2 = eq + (1.0 + eq) * eg + 2e-12;
+      if ((flags & 1u) && row_sgt) {
+        const double t = gld(row_sgt + i);
+        if (s2 - E2 > t || s2 + E2 < t) {
+          if (s2 - E2 > t && lane == 0) gadd(row_cnt + i, 1);
+          flags &= ~1u;
+        }
+      }
+      if ((flags & 2u) && col_sgt) {
+        const double t = gld(col_sgt + j);
+        if (s2 - E2 > t || s2 + E2 < t) {
+          if (s2 - E2 > t && lane == 0) gadd(col_cnt + j, 1);
+          flags &= ~2u;
+        }
+      }
+    }
+    if (!flags) continue;  // (decided at level 2, or a null entry)
     double rs = 0.0, cs = 0.0;
     if (PREFETCH) {
-      rs = ((flags & 1u) && row_sgt) ? row_sgt[i] : 0.0;
-      cs = ((flags & 2u) && col_sgt) ? col_sgt[j] : 0.0;
+      rs = ((flags & 1u) && row_sgt) ? gld(row_sgt + i) : 0.0;
+      cs = ((flags & 2u) && col_sgt) ? gld(col_sgt + j) : 0.0;
     }
-    const double s = wave_cos64(qraw + i * ldq, graw + j * ldg, qinv[i], ginv[j], d, lane);
+    const double s = wave_cos64(qraw + i * ldq, graw + j * ldg, gld(qinv + i), gld(ginv + j), d, lane);
     if (lane == 0) {
-      if ((flags & 1u) && row_sgt && s > (PREFETCH ? rs : row_sgt[i])) atomicAdd(&row_cnt[i], 1);
-      if ((flags & 2u) && col_sgt && s > (PREFETCH ? cs : col_sgt[j])) atomicAdd(&col_cnt[j], 1);
+      if ((flags & 1u) && row_sgt && s > (PREFETCH ? rs : gld(row_sgt + i))) gadd(row_cnt + i, 1);
+      if ((flags & 2u) && col_sgt && s > (PREFETCH ? cs : gld(col_sgt + j))) gadd(col_cnt + j, 1);
     }
   }
 }

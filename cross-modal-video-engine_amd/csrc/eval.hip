@@ -616,15 +616,114 @@ constexpr int FIX_NT = 256;
 #ifndef CMVE_FIX_BLOCKS
 #define CMVE_FIX_BLOCKS 1024
 #endif
+#ifndef CMVE_FIXB_BLOCKS
+#define CMVE_FIXB_BLOCKS 192  // (x 4 waves x 2 pairs: ~1,600 listed pairs of a 1k-A evaluation in one step)
+#endif
 
+// the fix-up of an evaluation with the level-2 planes (d_pad <= 1024): one flat walk over the buckets, TWO listed
+// pairs per wave per step with every level-2 load of both in flight (one round trip of 16 KiB), the directions
+// whose GT score lies outside s2 +- E2 decided there, fp64 (wave_cos64) for the few left
 template <typename TQ, typename TG>
-__global__ __launch_bounds__(FIX_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+__device__ __forceinline__ void eval_fix2_walk(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nb = c.nb, ldk = c.d_pad;
+  if (wave == 0) fixup_prefix(c.cand, nb, c.cap_b, 0, 1, nb, lane, pre);
+  __syncthreads();
+  const int64_t total = pre[nb];
+  const int nw = (int)(blockDim.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * nw * 2;
+  int64_t kb = 0;
+  auto entry = [&](int64_t cc) -> uint64_t {  // pair cc of the walk (0: none); cc increases call by call
+    if (cc >= total) return 0ull;
+    if (pre[kb + 1] <= cc) {
+      int64_t lo = kb + 1, hi = nb - 1;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= cc) lo = mid;
+        else hi = mid - 1;
+      }
+      kb = lo;
+    }
+    return gld(c.cand + nb + kb * c.cap_b + (cc - pre[kb]));
+  };
+  const bool dq = q.off != nullptr, dg = g.off != nullptr;
+  for (int64_t c0 = ((int64_t)blockIdx.x * nw + wave) * 2; c0 < total; c0 += stride) {
+    const uint64_t u[2] = {entry(c0), entry(c0 + 1)};
+    int64_t pi[2], pj[2];
+    uint32_t fl[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      pi[t] = (int64_t)(u[t] & 0x7fffffffull);
+      pj[t] = (int64_t)((u[t] >> 31) & 0x7fffffffull);
+      fl[t] = (uint32_t)(u[t] >> 62) & ((dq ? 1u : 0u) | (dg ? 2u : 0u));
+    }
+    double s2[2] = {0.0, 0.0};
+    const int64_t k = 16 * (int64_t)lane;
+    if (k < ldk) {
+      L16Frag fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        l16_load(q.h16 + pi[t] * ldk, q.lo16 + pi[t] * ldk, k, fa[t]);  // (a null entry reads row 0: harmless)
+        l16_load(g.h16 + pj[t] * ldk, g.lo16 + pj[t] * ldk, k, fb[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) s2[t] = l16_partial(fa[t], fb[t], 0.0);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s2[0] += __shfl_xor(s2[0], o, 64);
+      s2[1] += __shfl_xor(s2[1], o, 64);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (!fl[t]) continue;  // (wave-uniform)
+      const double eq = (double)gld(q.err_lo16 + pi[t]), eg = (double)gld(g.err_lo16 + pj[t]);
+      const double E2 = eq + (1.0 + eq) * eg + 2e-12;
+      const double tq = (fl[t] & 1u) ? gld(q.sgt + pi[t]) : 0.0, tg = (fl[t] & 2u) ? gld(g.sgt + pj[t]) : 0.0;
+      if ((fl[t] & 1u) && (s2[t] - E2 > tq || s2[t] + E2 < tq)) {
+        if (s2[t] - E2 > tq && lane == 0) gadd(q.cnt + pi[t], 1);
+        fl[t] &= ~1u;
+      }
+      if ((fl[t] & 2u) && (s2[t] - E2 > tg || s2[t] + E2 < tg)) {
+        if (s2[t] - E2 > tg && lane == 0) gadd(g.cnt + pj[t], 1);
+        fl[t] &= ~2u;
+      }
+      if (!fl[t]) continue;
+      // level 3: fp64, the fix-up's arithmetic
+      const double sc = wave_cos64((const TQ*)q.raw + pi[t] * q.ld, (const TG*)g.raw + pj[t] * g.ld,
+                                   gld(q.inv + pi[t]), gld(g.inv + pj[t]), c.d, lane);
+      if (lane == 0) {
+        if ((fl[t] & 1u) && sc > tq) gadd(q.cnt + pi[t], 1);
+        if ((fl[t] & 2u) && sc > tg) gadd(g.cnt + pj[t], 1);
+      }
+    }
+  }
+}
+
+// the evaluation's fix-up: the listed undecided pairs -- with the level-2 planes eval_fix2_walk, else fp64
+// (fixup_walk's flat walk)
+template <typename TQ, typename TG>
+__device__ __forceinline__ void eval_fix_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
   EVAL_STAMP(c, 2, 0);
-  if (!(c.dbg & 8))
+  if (c.dbg & 8) {
+  } else if (q.lo16 && g.lo16 && c.nb <= FIXUP_MAX_BUCKETS_PER_XCD) {
+    eval_fix2_walk<TQ, TG>(q, g, c);
+  } else {
     fixup_walk<TQ, TG, true>((const TQ*)q.raw, q.ld, q.inv, (const TG*)g.raw, g.ld, g.inv, c.d, q.off ? q.sgt : nullptr,
                              g.off ? g.sgt : nullptr, q.cnt, g.cnt, c.cand, c.nb, c.cap_b,
                              c.nb <= FIXUP_MAX_BUCKETS_PER_XCD);
+  }
   EVAL_STAMP(c, 2, 1);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(FIX_NT) void eval_fix_kernel(EvalSide q, EvalSide g, EvalCommon c) {
+  eval_fix_body<TQ, TG>(q, g, c);
+}
+template <typename TQ, typename TG>
+__global__ __launch_bounds__(FIX_NT) void eval_fix_batch_kernel(const EvalItem* __restrict__ tab) {
+  const EvalItem& it = tab[blockIdx.y];
+  eval_fix_body<TQ, TG>(it.q, it.g, it.c);
 }
 
 // the pair total / overflow size (cand_finalize_kernel's), one block
@@ -814,6 +913,12 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
     const unsigned blocks = (unsigned)((q.n_pad + g.n_pad + PREP_NW - 1) / PREP_NW);
     cmve::launch(eval_prep_batch_kernel<TQ, TG>, dim3(blocks, (unsigned)count), dim3(PREP_NT), 0u, s, tab);
     return check_launch("eval_prep_batch_kernel");
+  }
+  if (phase == 1) {
+    // the batch's fix-up: CMVE_FIXB_BLOCKS blocks of 4 waves per evaluation (~1,600 listed pairs at 1k-A)
+    cmve::launch(eval_fix_batch_kernel<TQ, TG>, dim3((unsigned)CMVE_FIXB_BLOCKS, (unsigned)count), dim3(FIX_NT), 0u,
+                 s, tab);
+    return check_launch("eval_fix_batch_kernel");
   }
   if (phase == 3) {
     const unsigned blocks = (unsigned)((q.n_pad + PREP_NW - 1) / PREP_NW);

@@ -276,7 +276,9 @@ __device__ __forceinline__ float wave_sum_f32(float v) {  // every lane gets the
   return (r0 + r1) + (r2 + r3);
 }
 
-template <int E, int HW, int NWV>  // HW heads per wave, NWV waves per block (one query): H = HW * NWV
+template <int E, int HW, int NWV, int R>  // HW heads per wave, NWV waves per block (one query): H = HW * NWV;
+// R key rows per step: their loads in flight together, their 2 + HW wave sums each interleaved (the online softmax
+// still takes the rows one by one, so the result does not depend on R)
 __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __restrict__ y, int64_t ldy, int npix, int cpr,
                                                           int L, int f, int gs, const float* __restrict__ u,
                                                           int64_t ldu, float eps, float* __restrict__ z, int64_t ldz,
@@ -287,12 +289,22 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
   const int64_t qb = blockIdx.x;
   const int64_t g = qb / gs, bb = qb - g * gs;
   const int T = f * L, cpr2 = cpr >> 1;
-  int64_t off[E2];  // this lane's float2 pieces of a key run: pixel p, channel pair c2
+  int off[E2];  // this lane's float2 pieces of a key run: pixel p, channel pair c2 (byte offsets < 2^31)
 #pragma unroll
   for (int m = 0; m < E2; ++m) {
     const int fi = lane + 64 * m, p = fi / cpr2, c2 = fi - p * cpr2;
-    off[m] = (int64_t)p * ldy + 2 * c2;
+    off[m] = 4 * (p * (int)ldy + 2 * c2);
   }
+  const int span = 4 * (int)((npix - 1) * ldy + cpr);  // a key run's byte span from its first element
+  typedef float mha_f32x2 __attribute__((ext_vector_type(2)));
+  auto load_run = [&](const float* base, float2 (&v)[E2]) {  // buffer loads: the run base in SGPRs, 32-bit offsets
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, span, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < E2; ++m) {
+      const mha_f32x2 w = __builtin_bit_cast(mha_f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off[m], 0, 0));
+      v[m] = make_float2(w.x, w.y);
+    }
+  };
   float uu[H][E];
 #pragma unroll
   for (int h = 0; h < H; ++h)
@@ -303,9 +315,9 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
       uu[h][2 * m + 1] = w.y;
     }
   auto row_base = [&](int t) {
-    const int64_t R = (int64_t)t * gs + bb;
-    const int64_t bf = g * gs * f + R / L;
-    return y + bf * npix * ldy + (R % L) * cpr;
+    const int64_t Rw = (int64_t)t * gs + bb;
+    const int64_t bf = g * gs * f + Rw / L;
+    return y + bf * npix * ldy + (Rw % L) * cpr;
   };
   float acc[H][E], mx[H], sm[H], vs[E];
 #pragma unroll
@@ -317,61 +329,75 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) vs[e] = 0.f;
-  float2 nxt[E2];
-  {
-    const float* b0 = row_base(0);
+  float2 nxt[R][E2];
 #pragma unroll
-    for (int m = 0; m < E2; ++m) nxt[m] = *(const float2*)(b0 + off[m]);
-  }
-  for (int t = 0; t < T; ++t) {
-    float x[E];
+  for (int r = 0; r < R; ++r) load_run(row_base(r), nxt[r]);
+  for (int t0 = 0; t0 < T; t0 += R) {
+    float x[R][E];
 #pragma unroll
-    for (int m = 0; m < E2; ++m) {
-      x[2 * m] = nxt[m].x;
-      x[2 * m + 1] = nxt[m].y;
-    }
-    if (t + 1 < T) {  // the next key row's loads in flight behind this row's arithmetic
-      const float* bn = row_base(t + 1);
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int m = 0; m < E2; ++m) nxt[m] = *(const float2*)(bn + off[m]);
-    }
-    float s = 0.f;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      s += x[e];
-      vs[e] += x[e];
-    }
-    const float mean = wave_sum_f32(s) / (float)D;
-    float c[E], q = 0.f, dot[H];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      c[e] = x[e] - mean;
-      q = fmaf(c[e], c[e], q);
-    }
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float a = 0.f;
-#pragma unroll
-      for (int e = 0; e < E; ++e) a = fmaf(c[e], uu[h][e], a);
-      dot[h] = a;
-    }
-    const float rstd = 1.0f / sqrtf(wave_sum_f32(q) / (float)D + eps);
-#pragma unroll
-    for (int e = 0; e < E; ++e) c[e] *= rstd;
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      const float sc = wave_sum_f32(dot[h]) * rstd;  // wave-uniform
-      if (sc > mx[h]) {
-        const float k = expf(mx[h] - sc);  // 0 on the first row
-        sm[h] *= k;
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[h][e] *= k;
-        mx[h] = sc;
+      for (int m = 0; m < E2; ++m) {
+        x[r][2 * m] = nxt[r][m].x;
+        x[r][2 * m + 1] = nxt[r][m].y;
       }
-      const float p = expf(sc - mx[h]);
-      sm[h] += p;
+    if (t0 + R < T) {  // the next R key rows' loads in flight behind these rows' arithmetic
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, c[e], acc[h][e]);
+      for (int r = 0; r < R; ++r) load_run(row_base(t0 + R + r), nxt[r]);
+    }
+    float s[R], mean[R], q[R], rstd[R], dot[R][H];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      s[r] = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        s[r] += x[r][e];
+        vs[e] += x[r][e];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) mean[r] = wave_sum_f32(s[r]) / (float)D;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      q[r] = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        x[r][e] -= mean[r];
+        q[r] = fmaf(x[r][e], x[r][e], q[r]);
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float a = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) a = fmaf(x[r][e], uu[h][e], a);
+        dot[r][h] = a;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      rstd[r] = 1.0f / sqrtf(wave_sum_f32(q[r]) / (float)D + eps);
+#pragma unroll
+      for (int h = 0; h < H; ++h) dot[r][h] = wave_sum_f32(dot[r][h]) * rstd[r];  // wave-uniform scores
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[r][e] *= rstd[r];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float sc = dot[r][h];
+        if (sc > mx[h]) {
+          const float k = expf(mx[h] - sc);  // 0 on the first row
+          sm[h] *= k;
+#pragma unroll
+          for (int e = 0; e < E; ++e) acc[h][e] *= k;
+          mx[h] = sc;
+        }
+        const float p = expf(sc - mx[h]);
+        sm[h] += p;
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, x[r][e], acc[h][e]);
+      }
     }
   }
 #pragma unroll
@@ -630,14 +656,34 @@ extern "C" int cmve_mha_absorbed(cmve_handle_t h, const float* y, int64_t ldy, i
                "cmve_mha_absorbed: strides / 8-byte alignment");
   if (B == 0) return CMVE_OK;
   const int cpr = (int)(d / npix), L = (int)(C / cpr);
-  if (d == 640 && H == 8) {  // the Combiner: d 640 = 64 lanes x 10, 8 heads
-    hipLaunchKernelGGL((mha_absorbed_kernel<10, 4, 2>), dim3((unsigned)B), dim3(128), 0, h->stream, y, ldy, (int)npix, cpr,
-                       L, (int)f, (int)gs, u, ldu, (float)eps, z, ldz, vmean, ldv);
-    return check_launch("mha_absorbed");
-  }
-  if (d == 512 && H == 8) {
-    hipLaunchKernelGGL((mha_absorbed_kernel<8, 4, 2>), dim3((unsigned)B), dim3(128), 0, h->stream, y, ldy, (int)npix, cpr,
-                       L, (int)f, (int)gs, u, ldu, (float)eps, z, ldz, vmean, ldv);
+  CMVE_REQUIRE(4 * npix * ldy < ((int64_t)1 << 31), "cmve_mha_absorbed: a key block's span exceeds 2 GiB");
+  static const int rows = [] {  // key rows per step (1, 2 or 4; study knob CMVE_MHA_ROWS)
+    const char* e = getenv("CMVE_MHA_ROWS");
+    const int r = e ? atoi(e) : 4;
+    return (r == 1 || r == 2) ? r : 4;
+  }();
+  static const int hpw = [] {  // heads per wave (4: two waves per query, 2: four; study knob CMVE_MHA_HPW)
+    const char* e = getenv("CMVE_MHA_HPW");
+    return (e && atoi(e) == 4) ? 4 : 2;
+  }();
+  const int T = (int)(f * L), R = (T % rows == 0) ? rows : ((T % 2 == 0) ? 2 : 1);
+#define CMVE_MHA_LAUNCH(E_, HW_, R_)                                                                                 \
+  hipLaunchKernelGGL((mha_absorbed_kernel<E_, HW_, 8 / HW_, R_>), dim3((unsigned)B), dim3(64 * (8 / HW_)), 0,         \
+                     h->stream, y, ldy, (int)npix, cpr, L, (int)f, (int)gs, u, ldu, (float)eps, z, ldz, vmean, ldv)
+#define CMVE_MHA_R(E_, HW_)             \
+  if (R == 4) CMVE_MHA_LAUNCH(E_, HW_, 4); \
+  else if (R == 2) CMVE_MHA_LAUNCH(E_, HW_, 2); \
+  else CMVE_MHA_LAUNCH(E_, HW_, 1)
+  if ((d == 640 || d == 512) && H == 8) {  // the Combiner: d 640 = 64 lanes x 10, 8 heads
+    if (d == 640) {
+      if (hpw == 4) { CMVE_MHA_R(10, 4); }
+      else { CMVE_MHA_R(10, 2); }
+    } else {
+      if (hpw == 4) { CMVE_MHA_R(8, 4); }
+      else { CMVE_MHA_R(8, 2); }
+    }
+#undef CMVE_MHA_R
+#undef CMVE_MHA_LAUNCH
     return check_launch("mha_absorbed");
   }
   set_error("cmve_mha_absorbed: instantiated for (d, H) = (640, 8), (512, 8)");

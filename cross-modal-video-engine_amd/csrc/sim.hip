@@ -103,6 +103,7 @@ struct SimArgs {
   // ghi) and their per-row bounds; a band pair is decided from h16 + lo16 (lo16_elem) when its score clears the
   // GT score by the level-2 bound; the rest go to the level-3 list (EvalCommon::l3, re-scored in fp64 by the
   // finish), or are re-scored here when it is full.  nullptr: every pair in fp64 here
+  int ovf_inline;  // K14 with a fix-up launch: a wave whose pairs overflow its bucket re-scores them itself
   const uint16_t* q_lo16;
   const uint16_t* g_lo16;
   const float* q_el;
@@ -112,38 +113,7 @@ struct SimArgs {
   int l3_cap;
 };
 
-// ---- K14 level-2 re-score: one pair's score from the fp16 + bf16 residual planes (lo16_elem, cmve_internal.h) ----
-// lane L holds elements [16L, 16L + 16) of each 1024-element chunk: two 16-B fp16 loads and two 16-B bf16 loads
-// per row and chunk.  x2 = h + lo is formed in fp64 (exact unless lo lies 2^-42 below h: then within 2^-53 |x2|),
-// the products and sums in fp64, so the sum's error is a few ulps of 1:
-//   |s2 - cos64| <= el_q + (1 + el_q) el_g + 2e-12
-// (the 2e-12 covers the fp64 sums here and in cos64, as score_error_bound's 1e-12 does for the MFMA bound)
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-struct L16Frag {
-  u32x4_t h0, h1, l0, l1;
-};
-__device__ __forceinline__ void l16_load(const uint16_t* __restrict__ hrow, const uint16_t* __restrict__ lrow,
-                                         int64_t k, L16Frag& f) {
-  f.h0 = gld((const u32x4_t*)(hrow + k));
-  f.h1 = gld((const u32x4_t*)(hrow + k + 8));
-  f.l0 = gld((const u32x4_t*)(lrow + k));
-  f.l1 = gld((const u32x4_t*)(lrow + k + 8));
-}
-__device__ __forceinline__ double l16_x(uint32_t hw, uint32_t lw, int half) {
-  const uint16_t h = (uint16_t)(hw >> (16 * half));
-  const uint32_t l = half ? (lw & 0xffff0000u) : (lw << 16);
-  return (double)(float)__builtin_bit_cast(_Float16, h) + (double)__uint_as_float(l);
-}
-__device__ __forceinline__ double l16_partial(const L16Frag& a, const L16Frag& b, double acc) {
-  const uint32_t ah[8] = {a.h0.x, a.h0.y, a.h0.z, a.h0.w, a.h1.x, a.h1.y, a.h1.z, a.h1.w};
-  const uint32_t al[8] = {a.l0.x, a.l0.y, a.l0.z, a.l0.w, a.l1.x, a.l1.y, a.l1.z, a.l1.w};
-  const uint32_t bh[8] = {b.h0.x, b.h0.y, b.h0.z, b.h0.w, b.h1.x, b.h1.y, b.h1.z, b.h1.w};
-  const uint32_t bl[8] = {b.l0.x, b.l0.y, b.l0.z, b.l0.w, b.l1.x, b.l1.y, b.l1.z, b.l1.w};
-#pragma unroll
-  for (int e = 0; e < 16; ++e)
-    acc = fma(l16_x(ah[e >> 1], al[e >> 1], e & 1), l16_x(bh[e >> 1], bl[e >> 1], e & 1), acc);
-  return acc;
-}
+// (L16Frag, l16_load, l16_partial: the level-2 re-score's fragments, cmve_internal.h)
 // the wave's level-2 scores of P pairs (rows qr[p] of the query planes, gc[p] of the gallery planes), every
 // load of all P pairs in flight before the sums; d_pad % 64 == 0 (a lane's 16 elements are all in or all out)
 template <int P>
@@ -1061,7 +1031,13 @@ void sim_kernel(
       if (inl && total && lane == 0) gadd(a.bucket_cnt + bucket, (unsigned long long)total);  // (no return)
       const bool emit = total != 0u && !inl;  // (inline: re-scored above; the bucket count is the pair total)
       if (emit) {
-        unsigned long long slot = __shfl(wbase, 0, 64) + excl;
+        const unsigned long long w0 = __shfl(wbase, 0, 64);  // this wave's first slot in the bucket
+        // K14 with a fix-up launch (SimArgs::ovf_inline): a wave whose pairs do not all fit its bucket re-scores
+        // them here in fp64 (into the global counts, after the flush) and leaves null entries in the slots it
+        // reserved -- an evaluation never overflows (tiles dense with undecided pairs: near-duplicate rows)
+        bool rescue = false;
+        if constexpr (INL) rescue = a.ovf_inline && w0 + total > (unsigned long long)a.cap_b;
+        unsigned long long slot = w0 + excl;
         unsigned long long* dst = a.cand + (size_t)bucket * a.cap_b;
   #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -1082,11 +1058,45 @@ void sim_kernel(
                        (unsigned long long)(cbase + (bit >> 2) * 16);
             } else {
               const unsigned long long flags = ((und[i] >> bit) & 1u) | (((und[i] >> (16 + bit)) & 1u) << 1);
-              packed = (unsigned long long)(rbase + i * 16 + (bit & 3)) |
-                       ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
+              packed = rescue ? 0ull
+                              : (unsigned long long)(rbase + i * 16 + (bit & 3)) |
+                                    ((unsigned long long)(cbase + (bit >> 2) * 16) << 31) | (flags << 62);
             }
             if ((long long)slot < a.cap_b) gst(dst + slot, packed);
             ++slot;
+          }
+        }
+        if constexpr (INL) {
+          if (rescue) {  // (wave-uniform) the wave's pairs one at a time: fixup_walk's arithmetic, global counts
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              uint32_t bits = (und[i] | (und[i] >> 16)) & 0xffffu;
+              unsigned long long mm;
+              while ((mm = __builtin_amdgcn_ballot_w64(bits != 0u))) {
+                const int src = (int)__builtin_ctzll(mm);
+                const uint32_t sb = (uint32_t)__builtin_amdgcn_readlane((int)bits, src);
+                const uint32_t su = (uint32_t)__builtin_amdgcn_readlane((int)und[i], src);
+                const int bit = __builtin_ctz(sb);
+                if (lane == src) bits &= bits - 1u;
+                const int64_t row = m0 + wr * (TM * 16) + (src >> 4) * 4 + i * 16 + (bit & 3);
+                const int64_t col = n0 + wc * (TN * 16) + (src & 15) + (bit >> 2) * 16;
+                const double inva = gld(a.q_inv + row), invb = gld(a.g_inv + col);
+                double sc;
+                if (a.q_f64) {
+                  const double* x = (const double*)a.q_raw + row * a.q_ld;
+                  sc = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane);
+                } else {
+                  const float* x = (const float*)a.q_raw + row * a.q_ld;
+                  sc = a.g_f64 ? wave_cos64(x, (const double*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane)
+                               : wave_cos64(x, (const float*)a.g_raw + col * a.g_ld, inva, invb, a.d, lane);
+                }
+                if (lane == 0) {
+                  if (((su >> bit) & 1u) && sc > gld(a.row_sgt + row)) gadd(a.row_cnt + row, 1);
+                  if (((su >> (16 + bit)) & 1u) && sc > gld(a.col_sgt + col)) gadd(a.col_cnt + col, 1);
+                }
+              }
+            }
           }
         }
       }
@@ -1980,6 +1990,7 @@ struct EvalPlan {
   SimArgs a;
   int qf, gf;
   bool paired, inline_fix;
+  bool fix_launch = false;  // (inline_fix sizes) the GEMM lists its undecided pairs for a fix-up launch (level 2 + fp64)
 };
 
 static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, const int64_t* row_off,
@@ -2093,13 +2104,22 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   const bool no_inline = fix_env && atoi(fix_env) != 0;
   P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
   // level-2 re-score from the fp16 + bf16 residual planes: the F16 mode whose prep runs the register path (the
-  // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides); level 3 deferred to the finish through
-  // the workspace's list.  CMVE_EVAL_NO_L2 (tests / kernel studies): every band pair in fp64 in the GEMM
+  // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides).  By default the rank GEMM only lists
+  // its undecided pairs and a fix-up launch re-scores them, one wave per pair (level 2, then fp64 for the few
+  // left): the GEMM's epilogue holds no round trip.  CMVE_EVAL_INLINE_L2 (kernel studies): level 2 inside the
+  // GEMM, level 3 deferred to the finish through the workspace's list; CMVE_EVAL_NO_L2 (tests / kernel studies):
+  // every band pair in fp64 inside the GEMM
   static const bool no_l2 = [] {
     const char* e = getenv("CMVE_EVAL_NO_L2");
     return e && atoi(e) != 0;
   }();
-  if (P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2) {
+  static const bool inline_l2 = [] {
+    const char* e = getenv("CMVE_EVAL_INLINE_L2");
+    return e && atoi(e) != 0;
+  }();
+  const bool l2 = P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2;
+  P.fix_launch = l2 && !inline_l2;
+  if (l2) {
     P.sq.lo16 = (uint16_t*)(base + w.q_l16);
     P.sg.lo16 = (uint16_t*)(base + w.g_l16);
     P.sq.err_lo16 = (float*)(base + w.q_el);
@@ -2108,15 +2128,20 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     a.g_lo16 = P.sg.lo16;
     a.q_el = P.sq.err_lo16;
     a.g_el = P.sg.err_lo16;
-    c.l3_count = (unsigned*)(base + w.l3);
-    c.l3 = (uint64_t*)(base + w.l3 + 8);
-    c.l3_cap = EVAL_L3_CAP;
-    a.l3_count = c.l3_count;
-    a.l3 = (unsigned long long*)c.l3;
-    a.l3_cap = c.l3_cap;
+    if (!P.fix_launch) {
+      c.l3_count = (unsigned*)(base + w.l3);
+      c.l3 = (uint64_t*)(base + w.l3 + 8);
+      c.l3_cap = EVAL_L3_CAP;
+      a.l3_count = c.l3_count;
+      a.l3 = (unsigned long long*)c.l3;
+      a.l3_cap = c.l3_cap;
+    }
   }
   if (P.inline_fix) {
-    a.fix_inline = 1;
+    // fix_inline 1: the GEMM re-scores its undecided pairs; with the fix-up launch (2) it lists them and re-scores
+    // only the pairs of a wave whose bucket is full (SimArgs::ovf_inline): never an overflow either way
+    a.fix_inline = P.fix_launch ? 0 : 1;
+    a.ovf_inline = P.fix_launch ? 1 : 0;
     a.q_f64 = P.qf;
     a.g_f64 = P.gf;
     a.q_raw = q->raw;
@@ -2126,7 +2151,7 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     a.d = q->d;
     a.q_inv = q->inv_norm;
     a.g_inv = g->inv_norm;
-    c.fix_inline = 1;
+    c.fix_inline = P.fix_launch ? 2 : 1;
   }
   a.dbg_stamps = c.stamps ? c.stamps + 3 * 1024 * 8 : nullptr;
   return CMVE_OK;
@@ -2176,8 +2201,8 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = P.inline_fix;
-  if (!P.inline_fix) {
+  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = P.inline_fix && !P.fix_launch;
+  if (!P.inline_fix || P.fix_launch) {
     arm(2);
     st = cmve::launch_eval(P.sq, P.sg, P.c, P.qf, P.gf, 1, s);
     if (st) return st;
@@ -2200,6 +2225,7 @@ struct cmve_eval_batch {
   int bm = 64, bn = 64;           // the rank tile (batch_geo_bm / _bn)
   cmve::EvalSide sq0, sg0;        // the shapes (the launch grids)
   cmve::EvalCommon c0;            // (the first evaluation's: which prep kernel applies)
+  bool fix_launch = false;        // the rank GEMM lists its undecided pairs for a fix-up launch
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
 };
@@ -2301,6 +2327,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;
   b->c0 = P0.c;
+  b->fix_launch = P0.fix_launch;
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
   if (e == hipSuccess) e = hipMalloc(&b->d_args, sizeof(SimArgs) * (size_t)count);
   if (e == hipSuccess)
@@ -2330,7 +2357,7 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
     kev = h->eval_kev[timing_slot];
     for (int k = 0; k < 8; ++k)
       if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
-    h->eval_no_fix[timing_slot] = true;
+    h->eval_no_fix[timing_slot] = !b->fix_launch;
   }
   auto arm = [&](int k) {
     if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
@@ -2349,6 +2376,11 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   }
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
+  if (b->fix_launch) {
+    arm(2);
+    st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 1, s);
+    if (st) return st;
+  }
   arm(3);
   st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, s);
   if (st) return st;

@@ -833,7 +833,7 @@ def test_rank_batch_stream_outs_timing(golden, torch_cuda):
             assert h[i, 9] == 0
             assert np.array_equal(h[i, 16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[i, 16 + n_q:], g["v2t_ranks"])
         ms = b.kernel_timing(0)
-        assert ms[0] > 0 and ms[1] > 0 and ms[2] == 0 and ms[3] > 0
+        assert ms[0] > 0 and ms[1] > 0 and ms[2] >= 0 and ms[3] > 0  # (fix-up: its own launch, or 0 inside the GEMM)
         b.close()
 
 

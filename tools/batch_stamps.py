@@ -59,7 +59,7 @@ def main():
         inflight = ((rel[:, 0][None, :] <= ts[:, None]) & (rel[:, 3][None, :] > ts[:, None])).sum(1)
         out["gemm"]["inflight_med"] = float(np.median(inflight))
         out["gemm"]["inflight_max"] = float(inflight.max())
-        for k, name in ((0, "prep"), (1, "finish")):
+        for k, name in ((0, "prep"), (1, "finish"), (2, "fix")):
             s = st[k]
             lv = s[:, 0] > 0
             if not lv.any():

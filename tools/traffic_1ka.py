@@ -31,9 +31,10 @@ def role(name):
     profile holding both never averages one into the other."""
     batch = "_batch_kernel" in name or ("sim_kernel<2, 1" in name and ", true>" in name)
     if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name or "eval_prep_pair_batch_kernel" in name \
-            or "eval_prep_batch_kernel" in name:
+            or "eval_prep_batch_kernel" in name or "eval_prep_pair_f16_kernel" in name \
+            or "eval_prep_pair_f16_batch_kernel" in name:
         r = "pack_gt_scores"
-    elif "eval_fix_kernel" in name:
+    elif "eval_fix_kernel" in name or "eval_fix_batch_kernel" in name:
         r = "fixup"
     elif "eval_finish_kernel" in name or "eval_finish_batch_kernel" in name:
         r = "ranks_recall"
