@@ -281,15 +281,17 @@ constexpr bool is_ring() {
 // (8 per wave per K-tile, ~2.7 us for the first 7 K-tiles of an 8-deep ring in the stamps), so a deeper
 // ring gains nothing alone, while 64 KiB lets two evaluations' rank GEMMs share a CU (two HIP streams:
 // 31.0 -> 26.6 us per evaluation, tools/eval_pipe.py)
-// The K14 batches' rings (cmve_eval_batch_*): 128 x 128 with 8 waves, 3 stages of 32 KiB (96 KiB + the epilogue
-// scratch: room beside it for another stream's prep blocks), and 128 x 64 (split-bf16), 3 stages of 24 KiB
+// The K14 batches' rings (cmve_eval_batch_*): 128 x 128 with 8 waves, 2 stages of 32 KiB -- two blocks per CU
+// (<= 128 VGPRs: CMVE_BATCH_WPE), so one block's level-2 re-score round trips run under the other's main loop
+// (round 4: rank GEMM 52 -> 38 us per batch of 8, headline 9.9e10 -> 1.11e11 against 3 stages of one block per
+// CU) -- and 128 x 64 (split-bf16), 3 stages of 24 KiB
 template <int MODE, int BM, int BN, bool PHASED, int NW = 4>
 constexpr int ring_stages() {
 #ifndef CMVE_G64_STAGES
 #define CMVE_G64_STAGES 4
 #endif
 #ifndef CMVE_G128R_STAGES
-#define CMVE_G128R_STAGES 3
+#define CMVE_G128R_STAGES 2
 #endif
   // (64 x 64, 128 x 64 and the 8-wave 128 x 128; the 4-wave G128 of mid-size problems keeps its 2-stage loop)
   return (PHASED || (BN != 64 && !(BM == 128 && BN == 128 && NW == 8)) || (BM != 64 && BM != 128))
@@ -1995,7 +1997,8 @@ struct EvalPlan {
 
 static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, const int64_t* row_off,
                         const int32_t* row_idx, const int64_t* col_off, const int32_t* col_idx, void* ws,
-                        int64_t ws_bytes, int64_t cand_cap, int64_t* out, const char* fn, EvalPlan& P) {
+                        int64_t ws_bytes, int64_t cand_cap, int64_t* out, const char* fn, EvalPlan& P,
+                        bool batch = false) {
   const int32_t mode = mode_flags & 0xff;
   const bool paired_req = (mode_flags & CMVE_EVAL_PAIRED) != 0;
   CMVE_REQUIRE((mode_flags & ~(0xff | CMVE_EVAL_PAIRED)) == 0, "%s: unknown flags 0x%x", fn, mode_flags);
@@ -2104,19 +2107,22 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   const bool no_inline = fix_env && atoi(fix_env) != 0;
   P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
   // level-2 re-score from the fp16 + bf16 residual planes: the F16 mode whose prep runs the register path (the
-  // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides).  By default the rank GEMM only lists
-  // its undecided pairs and a fix-up launch re-scores them, one wave per pair (level 2, then fp64 for the few
-  // left): the GEMM's epilogue holds no round trip.  CMVE_EVAL_INLINE_L2 (kernel studies): level 2 inside the
-  // GEMM, level 3 deferred to the finish through the workspace's list; CMVE_EVAL_NO_L2 (tests / kernel studies):
-  // every band pair in fp64 inside the GEMM
+  // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides).  Two forms: (a) inline (the default)
+  // -- level 2 inside the rank GEMM, level 3 deferred to the finish through the workspace's list; (b) the fix-up
+  // launch (CMVE_EVAL_INLINE_L2=0, kernel studies) -- the rank GEMM only lists its undecided pairs and eval_fix
+  // re-scores them, two pairs per wave.  Measured (round 4, tools/ab_env.sh, batches of 8): (b) takes the round
+  // trips out of the GEMM (38 -> 27 us) but its own launch costs 27 us -- its gathers miss the L2 the GEMM's
+  // tiles had just filled -- and a single evaluation pays a launch boundary (b2b 35.0 vs 35.9 us).
+  // CMVE_EVAL_NO_L2 (tests / kernel studies): every band pair in fp64 inside the GEMM
   static const bool no_l2 = [] {
     const char* e = getenv("CMVE_EVAL_NO_L2");
     return e && atoi(e) != 0;
   }();
-  static const bool inline_l2 = [] {
+  static const int inline_l2_env = [] {  // -1: the per-path default
     const char* e = getenv("CMVE_EVAL_INLINE_L2");
-    return e && atoi(e) != 0;
+    return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
+  const bool inline_l2 = inline_l2_env >= 0 ? inline_l2_env == 1 : true;
   const bool l2 = P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2;
   P.fix_launch = l2 && !inline_l2;
   if (l2) {
@@ -2286,7 +2292,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   for (int i = 0; i < count; ++i) {
     EvalPlan P;
     const int st = eval_prepare(q[i], g[i], mode_flags, row_off, row_idx, col_off, col_idx, ws[i], ws_bytes,
-                                cand_cap, out[i], "cmve_eval_batch_create", P);
+                                cand_cap, out[i], "cmve_eval_batch_create", P, true);
     if (st) return st;
     CMVE_REQUIRE(P.inline_fix, "cmve_eval_batch_create: batches take the G64 geometry (fewer than 128 tiles of "
                                "128^2, e.g. 1,000 x 1,000) with the inline fix-up");
