@@ -41,6 +41,11 @@ def element_wise_sum(image_features, text_features):
 
 def _as_int64(names) -> np.ndarray:
     """int(v) of every name (ints, numpy ints or numeric strings), vectorised when possible."""
+    if isinstance(names, (list, tuple)):
+        try:  # a list of Python ints: one pass, no intermediate object array
+            return np.fromiter(names, np.int64, len(names))
+        except (TypeError, ValueError, OverflowError):
+            pass
     a = np.asarray(names)
     if a.dtype.kind in "iu":
         return a.astype(np.int64, copy=False).reshape(-1)
@@ -56,11 +61,20 @@ class _NameIndex:
 
     def __init__(self, index_names: Sequence):
         keys = _as_int64(index_names)
+        self.lut = None
+        if keys.size and keys.min() >= 0 and keys.max() < 4 * keys.size + 1024:
+            # dense non-negative ids (the usual case): a direct table, the last row of a repeated id winning
+            self.lut = np.full(int(keys.max()) + 1, -1, np.int64)
+            np.maximum.at(self.lut, keys, np.arange(keys.size, dtype=np.int64))
+            return
         self.order = np.argsort(keys, kind="stable")
         self.sorted = keys[self.order]
 
     def rows(self, names: Sequence) -> np.ndarray:
         want = _as_int64(names)
+        if self.lut is not None:
+            ok = (want >= 0) & (want < self.lut.size)
+            return np.where(ok, self.lut[np.where(ok, want, 0)], -1)
         if self.sorted.size == 0:
             return np.full(want.shape, -1, np.int64)
         at = np.searchsorted(self.sorted, want, side="right") - 1

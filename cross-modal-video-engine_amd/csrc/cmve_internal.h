@@ -292,6 +292,14 @@ struct PackAcc {
   float e4 = 0.f;  // the bf16 residual plane's squared residuals (lo16_elem), summed in fp32
 };
 
+// block id -> its XCD's contiguous share of [0, total): the dispatcher deals blocks to the 8 XCDs round robin, so
+// XCD x (= bid & 7) walks its own contiguous range in dispatch order and neighbouring work items share its L2
+__device__ __forceinline__ int xcd_linear(int bid, int total) {
+  const int xcd = bid & 7, local = bid >> 3;
+  const int q = total >> 3, r = total & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
 // ---- the bf16 residual plane of the fp16 rank operand (K14 level-2 re-score) ----
 // An element x (fp64, normalised) is packed as xf = fp32(x), h = fp16(xf); d2 = xf - h is exact in fp32 and
 // lo = bf16(d2) (RNE) keeps its top 8 bits: x2 = h + lo with |x - x2| <= |x - xf| + |d2 - lo|, where

@@ -286,7 +286,9 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
   constexpr int D = 64 * E, E2 = E / 2, H = HW;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // heads [wv HW, (wv + 1) HW)
-  const int64_t qb = blockIdx.x;
+  // neighbouring queries of a group read neighbouring 160-B key runs of the same conv rows (their cache lines
+  // overlap): XCD-contiguous query ranges keep those lines in one L2 instead of fetching them into two or three
+  const int64_t qb = xcd_linear((int)blockIdx.x, (int)gridDim.x);
   const int64_t g = qb / gs, bb = qb - g * gs;
   const int T = f * L, cpr2 = cpr >> 1;
   int off[E2];  // this lane's float2 pieces of a key run: pixel p, channel pair c2 (byte offsets < 2^31)

@@ -140,13 +140,7 @@ __device__ __forceinline__ void l16_scores(const SimArgs& a, const int64_t (&qr)
     for (int p = 0; p < P; ++p) s2[p] += __shfl_xor(s2[p], o, 64);
 }
 
-// bijective XCD remap + grouped (GN gallery tiles x all query tiles) logical order
-// block id -> its XCD's contiguous share of [0, total): XCD x (= bid & 7) walks its own range in dispatch order
-__device__ __forceinline__ int xcd_linear(int bid, int total) {
-  const int xcd = bid & 7, local = bid >> 3;
-  const int q = total >> 3, r = total & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-}
+// bijective XCD remap (xcd_linear, cmve_internal.h) + grouped (GN gallery tiles x all query tiles) logical order
 __device__ __forceinline__ void tile_grouped(int L, int nblk_m, int nblk_n, int GN, int& bm, int& bn);
 __device__ __forceinline__ void tile_of_block(int bid, int nblk_m, int nblk_n, int GN, int& bm, int& bn) {
   tile_grouped(xcd_linear(bid, nblk_m * nblk_n), nblk_m, nblk_n, GN, bm, bn);
