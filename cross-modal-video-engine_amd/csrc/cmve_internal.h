@@ -345,6 +345,7 @@ __device__ __forceinline__ void pack_elem(double xh, bool want_f16, uint16_t& h,
 }
 
 typedef unsigned short cmve_u16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t cmve_u32x2 __attribute__((ext_vector_type(2)));
 
 // zero planes of a padding row (d_pad % 64 == 0)
 __device__ __forceinline__ void pack_pad_row(uint16_t* hrow, uint16_t* lrow, uint16_t* frow, int64_t d_pad,

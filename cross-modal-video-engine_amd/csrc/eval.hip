@@ -457,11 +457,22 @@ __device__ __forceinline__ void eval_prep_pair_body(const EvalSide& q, const Eva
 template <int NM>
 __device__ __forceinline__ void pack_f16_lo16(const EvalSide& A, int64_t row, const double (&v)[NM][4], double inv,
                                               int lane, bool store, double& e3, float& e4) {
+  // The planes are stored WRITE-THROUGH (sc1): their lines leave the XCD's L2 clean, so this launch's end-of-kernel
+  // release (buffer_wbl2) has ~8 MB per evaluation less to write back before the rank GEMM may start
+  // (MI355X_MICROARCH.md, visibility: a release costs ~1.7 us clean, several us freshly dirtied; the eval stamps
+  // measured a 5.3 us gap between the last prep block and the first rank-GEMM block).  16-B sc1 stores cost what
+  // plain ones do, narrower ones several times more, so lanes L and L ^ 1 swap halves of two chunks (one DPP swap
+  // per dword) and each stores 16 contiguous bytes: the even lane chunk m's [4L, 4L + 8), the odd lane chunk m + 1's
+  // [4L - 4, 4L + 4).
   uint16_t* frow = A.h16 + row * (int64_t)(NM * 256);
   uint16_t* lrow = A.lo16 + row * (int64_t)(NM * 256);
+  const __amdgpu_buffer_rsrc_t rf = __builtin_amdgcn_make_buffer_rsrc((void*)frow, 0, NM * 512, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)lrow, 0, NM * 512, 0x00020000);
+  const bool odd = lane & 1;
+  cmve_u32x2 pf = {0u, 0u}, pl = {0u, 0u};  // an even chunk's values, held for its pair
+  auto swap = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false); };
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    const int64_t k = (int64_t)lane * 4 + 256 * m;
     cmve_u16x4 fv, lv;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -478,9 +489,23 @@ __device__ __forceinline__ void pack_f16_lo16(const EvalSide& A, int64_t row, co
       fv[q] = __builtin_bit_cast(uint16_t, h);
       lv[q] = __builtin_bit_cast(uint16_t, lo);
     }
+    const cmve_u32x2 f2 = __builtin_bit_cast(cmve_u32x2, fv), l2 = __builtin_bit_cast(cmve_u32x2, lv);
     if (store) {
-      gst((cmve_u16x4*)(frow + k), fv);
-      gst((cmve_u16x4*)(lrow + k), lv);
+      if ((m & 1) == 0 && m + 1 < NM) {
+        pf = f2;
+        pl = l2;
+      } else if (m & 1) {
+        const cmve_u32x2 sf = odd ? pf : f2, sl = odd ? pl : l2;  // what the partner lane needs
+        const cmve_u32x2 rf2 = {swap(sf.x), swap(sf.y)}, rl2 = {swap(sl.x), swap(sl.y)};
+        const cmve_u32x4 df = odd ? cmve_u32x4{rf2.x, rf2.y, f2.x, f2.y} : cmve_u32x4{pf.x, pf.y, rf2.x, rf2.y};
+        const cmve_u32x4 dl = odd ? cmve_u32x4{rl2.x, rl2.y, l2.x, l2.y} : cmve_u32x4{pl.x, pl.y, rl2.x, rl2.y};
+        const int off = odd ? (m * 256 + 4 * (lane - 1)) * 2 : ((m - 1) * 256 + 4 * lane) * 2;
+        __builtin_amdgcn_raw_buffer_store_b128(df, rf, off, 0, 16);  // (aux 16: sc1)
+        __builtin_amdgcn_raw_buffer_store_b128(dl, rl, off, 0, 16);
+      } else {  // the last chunk of an odd NM: 8 B per lane
+        __builtin_amdgcn_raw_buffer_store_b64(f2, rf, (m * 256 + 4 * lane) * 2, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b64(l2, rl, (m * 256 + 4 * lane) * 2, 0, 16);
+      }
     }
     // the chunk's residual sums complete here (left free, the compiler sank every fma chain below the last
     // chunk's stores and held all 32 elements' temporaries: ~190 registers)
@@ -785,14 +810,30 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
   // re-score) and added to this block's counts through LDS.  A pair listed for both directions is scored by
   // the block of its row and by the block of its column.
   __shared__ int add_q[FIN_NT], add_g[FIN_NT];
-  const unsigned n3 = c.l3_count ? min(gld(c.l3_count), (unsigned)c.l3_cap) : 0u;
+  // every load that does not depend on the level-3 pass first, with the list's count and each wave's first entry
+  // (read speculatively: the list holds l3_cap entries), so the pass adds one round trip instead of three
+  const bool hq = q.off && i < q.n, hg = g.off && i < g.n;
+  int cq = 0, cg = 0, g1 = 0;
+  double tq = 0.0, tg = 0.0;
+  if (hq) {
+    cq = gld(q.cnt + i);
+    tq = gld(q.sgt + i);
+    if (q.gt1) g1 = gld(q.gt1 + i);
+  }
+  if (hg) {
+    cg = gld(g.cnt + i);
+    tg = gld(g.sgt + i);
+  }
+  const bool l3 = c.l3_count != nullptr && FIN_NW <= c.l3_cap;
+  const unsigned n3 = l3 ? min(gld(c.l3_count), (unsigned)c.l3_cap) : 0u;
+  const uint64_t u_first = l3 ? gld(c.l3 + wave) : 0ull;
   if (n3) {
     add_q[threadIdx.x] = 0;
     add_g[threadIdx.x] = 0;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * FIN_NT;
     for (unsigned e = (unsigned)wave; e < n3; e += FIN_NW) {
-      const uint64_t u = gld(c.l3 + e);
+      const uint64_t u = e == (unsigned)wave ? u_first : gld(c.l3 + e);
       const int64_t pi = (int64_t)(u & 0x7fffffffull), pj = (int64_t)((u >> 31) & 0x7fffffffull);
       const unsigned fl = (unsigned)(u >> 62);
       const bool mq = (fl & 1u) && pi >= r0 && pi < r0 + FIN_NT;
@@ -809,15 +850,15 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
   }
   int64_t rq = 0, rg = 0;
   bool unpaired = false;  // a CMVE_EVAL_PAIRED row whose lists were not a one-to-one pairing (the paired prep)
-  if (q.off && i < q.n) {
-    rq = gt_rank_of(gld(q.cnt + i) + (n3 ? add_q[threadIdx.x] : 0), gld(q.sgt + i), g.n);
+  if (hq) {
+    rq = gt_rank_of(cq + (n3 ? add_q[threadIdx.x] : 0), tq, g.n);
     gst(q.ranks + i, rq);
-    unpaired = q.gt1 && gld(q.gt1 + i) == -2;
+    unpaired = q.gt1 && g1 == -2;
   }
   const unsigned long long unp = __builtin_amdgcn_ballot_w64(unpaired);
   if (unp && lane == 0) gadd((unsigned long long*)&c.stats[11], (unsigned long long)__builtin_popcountll(unp));
-  if (g.off && i < g.n) {
-    rg = gt_rank_of(gld(g.cnt + i) + (n3 ? add_g[threadIdx.x] : 0), gld(g.sgt + i), q.n);
+  if (hg) {
+    rg = gt_rank_of(cg + (n3 ? add_g[threadIdx.x] : 0), tg, q.n);
     gst(g.ranks + i, rg);
   }
   unsigned long long sq = (unsigned long long)rq, sg = (unsigned long long)rg;

@@ -316,10 +316,11 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
       uu[h][2 * m] = w.x;
       uu[h][2 * m + 1] = w.y;
     }
-  auto row_base = [&](int t) {
-    const int64_t Rw = (int64_t)t * gs + bb;
-    const int64_t bf = g * gs * f + Rw / L;
-    return y + bf * npix * ldy + (Rw % L) * cpr;
+  auto row_base = [&](int t) {  // (32-bit division: the int64 one carries a branch that splits the row loop)
+    const unsigned Rw = (unsigned)(t * gs + (int)bb), Lu = (unsigned)L;
+    const unsigned rq = Rw / Lu, rr = Rw - rq * Lu;
+    const int64_t bf = g * gs * f + (int64_t)rq;
+    return y + bf * npix * ldy + (int64_t)rr * cpr;
   };
   float acc[H][E], mx[H], sm[H], vs[E];
 #pragma unroll
@@ -331,22 +332,16 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) vs[e] = 0.f;
-  float2 nxt[R][E2];
-#pragma unroll
-  for (int r = 0; r < R; ++r) load_run(row_base(r), nxt[r]);
-  for (int t0 = 0; t0 < T; t0 += R) {
+  // one step: R key rows from buf (LayerNorm statistics, the HW head scores, the online softmax row by row)
+  auto step = [&](const float2 (&buf)[R][E2]) {
     float x[R][E];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int m = 0; m < E2; ++m) {
-        x[r][2 * m] = nxt[r][m].x;
-        x[r][2 * m + 1] = nxt[r][m].y;
+        x[r][2 * m] = buf[r][m].x;
+        x[r][2 * m + 1] = buf[r][m].y;
       }
-    if (t0 + R < T) {  // the next R key rows' loads in flight behind these rows' arithmetic
-#pragma unroll
-      for (int r = 0; r < R; ++r) load_run(row_base(t0 + R + r), nxt[r]);
-    }
     float s[R], mean[R], q[R], rstd[R], dot[R][H];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -387,21 +382,38 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
       for (int e = 0; e < E; ++e) x[r][e] *= rstd[r];
 #pragma unroll
       for (int h = 0; h < H; ++h) {
+        // branch-free online softmax (a branch per head split the step into blocks, and the compiler then sank the
+        // next rows' loads below them): k = 1 exactly when the maximum stays, so the rescale is a no-op there and
+        // the result equals the branchy form's bit for bit (rounded multiply, then add: no contraction)
         const float sc = dot[r][h];
-        if (sc > mx[h]) {
-          const float k = expf(mx[h] - sc);  // 0 on the first row
-          sm[h] *= k;
+        const float nm = fmaxf(mx[h], sc);
+        const float k = expf(mx[h] - nm);  // 0 on the first row (mx = -inf), 1 when sc <= mx
+        const float p = expf(sc - nm);
+        mx[h] = nm;
+        sm[h] = __fadd_rn(__fmul_rn(sm[h], k), p);
 #pragma unroll
-          for (int e = 0; e < E; ++e) acc[h][e] *= k;
-          mx[h] = sc;
-        }
-        const float p = expf(sc - mx[h]);
-        sm[h] += p;
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, x[r][e], acc[h][e]);
+        for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, x[r][e], __fmul_rn(acc[h][e], k));
       }
     }
+  };
+  auto issue = [&](int t, float2 (&buf)[R][E2]) {  // rows t .. t + R - 1 (past the last row: the last row again)
+#pragma unroll
+    for (int r = 0; r < R; ++r) load_run(row_base(min(t + r, T - 1)), buf[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // two named buffers in ping-pong (no register copy between a load and its use: with one prefetch buffer copied
+  // into the working rows, the compiler placed the copy -- and a wait for the prefetch -- at the loop's back edge,
+  // so every row waited out a full memory round trip)
+  float2 ba[R][E2], bb2[R][E2];
+  issue(0, ba);
+  int t0 = 0;
+  for (; t0 + 2 * R <= T; t0 += 2 * R) {
+    issue(t0 + R, bb2);
+    step(ba);
+    issue(t0 + 2 * R, ba);
+    step(bb2);
   }
+  if (t0 < T) step(ba);  // (T an odd multiple of R)
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     const float inv = 1.0f / sm[h];

@@ -355,6 +355,9 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_L2_P
 #define CMVE_L2_P 1  // K14 level-2 re-score: pairs per wave in flight at once (2: 128+ VGPRs, spills at 4 waves per SIMD)
 #endif
+#ifndef CMVE_L2_P_ONE
+#define CMVE_L2_P_ONE 2  // the same for one evaluation's G64 rank GEMM (4 waves, ~6 listed pairs per tile: one round)
+#endif
 // BATCH: one launch over a batch of same-shaped problems (cmve_eval_batch_*): the block picks the problem's
 // argument block in `tab` (see batch_item below); otherwise `tab` is unused
 #ifndef CMVE_BATCH_WPE
@@ -860,7 +863,7 @@ void sim_kernel(
               // direction left undecided goes to the level-3 list (fp64 in the finish launch, off this kernel's
               // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
               // entries: no other wave touches them)
-              constexpr int RP = CMVE_L2_P;
+              constexpr int RP = BATCH ? CMVE_L2_P : CMVE_L2_P_ONE;
               for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
                 int64_t qr[RP], gc[RP];
                 uint32_t ent[RP];
@@ -870,13 +873,21 @@ void sim_kernel(
                   qr[u] = m0 + (ent[u] & 0xff);
                   gc[u] = n0 + ((ent[u] >> 8) & 0xff);
                 }
+                // the pairs' row bounds are loaded with their plane rows (as a dependent load after the score
+                // they cost the re-score a second round trip)
+                float elq[RP], elg[RP];
+#pragma unroll
+                for (int u = 0; u < RP; ++u) {
+                  elq[u] = gld(a.q_el + qr[u]);
+                  elg[u] = gld(a.g_el + gc[u]);
+                }
                 double s2[RP];
                 l16_scores<RP>(a, qr, gc, lane, s2);
                 if (lane == 0) {
 #pragma unroll
                   for (int u = 0; u < RP; ++u) {
                     if (p0 + u >= ntot) break;
-                    const double eq = (double)gld(a.q_el + qr[u]), eg = (double)gld(a.g_el + gc[u]);
+                    const double eq = (double)elq[u], eg = (double)elg[u];
                     const double E2 = eq + (1.0 + eq) * eg + 2e-12;
                     uint32_t fl = (ent[u] >> 16) & 3u;
                     const int lr = (int)(ent[u] & 0xff), lc = (int)((ent[u] >> 8) & 0xff);
