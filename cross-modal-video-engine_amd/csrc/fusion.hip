@@ -277,13 +277,15 @@ __device__ __forceinline__ float wave_sum_f32(float v) {  // every lane gets the
 }
 
 template <int E, int HW, int NWV, int R>  // HW heads per wave, NWV waves per block (one query): H = HW * NWV;
-// R key rows per step: their loads in flight together, their 2 + HW wave sums each interleaved (the online softmax
-// still takes the rows one by one, so the result does not depend on R)
-__global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __restrict__ y, int64_t ldy, int npix, int cpr,
+// R key rows per step, their 2 + HW wave sums interleaved.  The lane's elements are handled in pairs on the packed
+// fp32 pipe (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of work per instruction): the kernel is
+// VALU-bound (~300 instructions per key row and wave before), not load-bound
+__global__ __launch_bounds__(64 * NWV, 3) void mha_absorbed_kernel(const float* __restrict__ y, int64_t ldy, int npix, int cpr,
                                                           int L, int f, int gs, const float* __restrict__ u,
                                                           int64_t ldu, float eps, float* __restrict__ z, int64_t ldz,
                                                           float* __restrict__ vmean, int64_t ldv) {
   constexpr int D = 64 * E, E2 = E / 2, H = HW;
+  typedef float f2v __attribute__((ext_vector_type(2)));
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // heads [wv HW, (wv + 1) HW)
   // neighbouring queries of a group read neighbouring 160-B key runs of the same conv rows (their cache lines
@@ -298,105 +300,88 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
     off[m] = 4 * (p * (int)ldy + 2 * c2);
   }
   const int span = 4 * (int)((npix - 1) * ldy + cpr);  // a key run's byte span from its first element
-  typedef float mha_f32x2 __attribute__((ext_vector_type(2)));
-  auto load_run = [&](const float* base, float2 (&v)[E2]) {  // buffer loads: the run base in SGPRs, 32-bit offsets
+  auto load_run = [&](const float* base, f2v (&v)[E2]) {  // buffer loads: the run base in SGPRs, 32-bit offsets
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, span, 0x00020000);
 #pragma unroll
-    for (int m = 0; m < E2; ++m) {
-      const mha_f32x2 w = __builtin_bit_cast(mha_f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, off[m], 0, 0));
-      v[m] = make_float2(w.x, w.y);
-    }
+    for (int m = 0; m < E2; ++m) v[m] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, off[m], 0, 0));
   };
-  float uu[H][E];
+  f2v uu[H][E2];
 #pragma unroll
   for (int h = 0; h < H; ++h)
 #pragma unroll
-    for (int m = 0; m < E2; ++m) {
-      const float2 w = *(const float2*)(u + qb * ldu + (wv * HW + h) * D + 2 * (lane + 64 * m));
-      uu[h][2 * m] = w.x;
-      uu[h][2 * m + 1] = w.y;
-    }
+    for (int m = 0; m < E2; ++m) uu[h][m] = *(const f2v*)(u + qb * ldu + (wv * HW + h) * D + 2 * (lane + 64 * m));
   auto row_base = [&](int t) {  // (32-bit division: the int64 one carries a branch that splits the row loop)
     const unsigned Rw = (unsigned)(t * gs + (int)bb), Lu = (unsigned)L;
     const unsigned rq = Rw / Lu, rr = Rw - rq * Lu;
     const int64_t bf = g * gs * f + (int64_t)rq;
     return y + bf * npix * ldy + (int64_t)rr * cpr;
   };
-  float acc[H][E], mx[H], sm[H], vs[E];
+  f2v acc[H][E2], vs[E2];
+  float mx[H], sm[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     mx[h] = -INFINITY;
     sm[h] = 0.f;
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[h][e] = 0.f;
+    for (int m = 0; m < E2; ++m) acc[h][m] = f2v{0.f, 0.f};
   }
 #pragma unroll
-  for (int e = 0; e < E; ++e) vs[e] = 0.f;
+  for (int m = 0; m < E2; ++m) vs[m] = f2v{0.f, 0.f};
   // one step: R key rows from buf (LayerNorm statistics, the HW head scores, the online softmax row by row)
-  auto step = [&](const float2 (&buf)[R][E2]) {
-    float x[R][E];
+  auto step = [&](f2v (&x)[R][E2]) {
+    float mean[R], rstd[R], dot[R][H];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r) {
+      f2v s2 = {0.f, 0.f};
 #pragma unroll
       for (int m = 0; m < E2; ++m) {
-        x[r][2 * m] = buf[r][m].x;
-        x[r][2 * m + 1] = buf[r][m].y;
+        s2 += x[r][m];
+        vs[m] += x[r][m];
       }
-    float s[R], mean[R], q[R], rstd[R], dot[R][H];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      s[r] = 0.f;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        s[r] += x[r][e];
-        vs[e] += x[r][e];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) mean[r] = wave_sum_f32(s[r]) / (float)D;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      q[r] = 0.f;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        x[r][e] -= mean[r];
-        q[r] = fmaf(x[r][e], x[r][e], q[r]);
-      }
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        float a = 0.f;
-#pragma unroll
-        for (int e = 0; e < E; ++e) a = fmaf(x[r][e], uu[h][e], a);
-        dot[r][h] = a;
-      }
+      mean[r] = wave_sum_f32(s2.x + s2.y) / (float)D;
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      rstd[r] = 1.0f / sqrtf(wave_sum_f32(q[r]) / (float)D + eps);
+      const f2v mn = {mean[r], mean[r]};
+      f2v q2 = {0.f, 0.f};
+      f2v a2[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) dot[r][h] = wave_sum_f32(dot[r][h]) * rstd[r];  // wave-uniform scores
+      for (int h = 0; h < H; ++h) a2[h] = f2v{0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < E2; ++m) {
+        x[r][m] -= mn;
+        q2 = __builtin_elementwise_fma(x[r][m], x[r][m], q2);
+#pragma unroll
+        for (int h = 0; h < H; ++h) a2[h] = __builtin_elementwise_fma(x[r][m], uu[h][m], a2[h]);
+      }
+      rstd[r] = 1.0f / sqrtf(wave_sum_f32(q2.x + q2.y) / (float)D + eps);
+#pragma unroll
+      for (int h = 0; h < H; ++h) dot[r][h] = wave_sum_f32(a2[h].x + a2[h].y) * rstd[r];  // wave-uniform scores
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+      const f2v rs2 = {rstd[r], rstd[r]};
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[r][e] *= rstd[r];
+      for (int m = 0; m < E2; ++m) x[r][m] *= rs2;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         // branch-free online softmax (a branch per head split the step into blocks, and the compiler then sank the
-        // next rows' loads below them): k = 1 exactly when the maximum stays, so the rescale is a no-op there and
-        // the result equals the branchy form's bit for bit (rounded multiply, then add: no contraction)
+        // next rows' loads below them): k = 1 exactly when the maximum stays, so the rescale is a no-op there;
+        // one exponential per head and row: with the new maximum nm = max(mx, sc), one of exp(mx - nm), exp(sc - nm)
+        // is exp(0) = 1 and the other is exp(-|sc - mx|) (exact negation: the same bits as computing it directly)
         const float sc = dot[r][h];
-        const float nm = fmaxf(mx[h], sc);
-        const float k = expf(mx[h] - nm);  // 0 on the first row (mx = -inf), 1 when sc <= mx
-        const float p = expf(sc - nm);
-        mx[h] = nm;
+        const bool up = sc > mx[h];
+        const float e = expf(up ? mx[h] - sc : sc - mx[h]);  // 0 on the first row (mx = -inf)
+        const float k = up ? e : 1.f, p = up ? 1.f : e;
+        mx[h] = up ? sc : mx[h];
         sm[h] = __fadd_rn(__fmul_rn(sm[h], k), p);
+        const f2v k2 = {k, k}, p2 = {p, p};
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc[h][e] = fmaf(p, x[r][e], __fmul_rn(acc[h][e], k));
+        for (int m = 0; m < E2; ++m) acc[h][m] = __builtin_elementwise_fma(p2, x[r][m], acc[h][m] * k2);
       }
     }
   };
-  auto issue = [&](int t, float2 (&buf)[R][E2]) {  // rows t .. t + R - 1 (past the last row: the last row again)
+  auto issue = [&](int t, f2v (&buf)[R][E2]) {  // rows t .. t + R - 1 (past the last row: the last row again)
 #pragma unroll
     for (int r = 0; r < R; ++r) load_run(row_base(min(t + r, T - 1)), buf[r]);
     __builtin_amdgcn_sched_barrier(0);
@@ -404,7 +389,7 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
   // two named buffers in ping-pong (no register copy between a load and its use: with one prefetch buffer copied
   // into the working rows, the compiler placed the copy -- and a wait for the prefetch -- at the loop's back edge,
   // so every row waited out a full memory round trip)
-  float2 ba[R][E2], bb2[R][E2];
+  f2v ba[R][E2], bb2[R][E2];
   issue(0, ba);
   int t0 = 0;
   for (; t0 + 2 * R <= T; t0 += 2 * R) {
@@ -417,18 +402,17 @@ __global__ __launch_bounds__(64 * NWV) void mha_absorbed_kernel(const float* __r
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     const float inv = 1.0f / sm[h];
+    const f2v i2 = {inv, inv};
 #pragma unroll
-    for (int m = 0; m < E2; ++m)
-      *(float2*)(z + qb * ldz + (wv * HW + h) * D + 2 * (lane + 64 * m)) =
-          make_float2(acc[h][2 * m] * inv, acc[h][2 * m + 1] * inv);
+    for (int m = 0; m < E2; ++m) *(f2v*)(z + qb * ldz + (wv * HW + h) * D + 2 * (lane + 64 * m)) = acc[h][m] * i2;
   }
   if (wv != 0) return;  // v.mean(0): wave 0's sums
   const float invT = 1.0f / (float)T;
 #pragma unroll
   for (int m = 0; m < E2; ++m) {
     const int fi = lane + 64 * m, p = fi / cpr2, c0 = 2 * (fi - p * cpr2);
-    vmean[qb * ldv + (int64_t)c0 * npix + p] = vs[2 * m] * invT;
-    vmean[qb * ldv + (int64_t)(c0 + 1) * npix + p] = vs[2 * m + 1] * invT;
+    vmean[qb * ldv + (int64_t)c0 * npix + p] = vs[m].x * invT;
+    vmean[qb * ldv + (int64_t)(c0 + 1) * npix + p] = vs[m].y * invT;
   }
 }
 
