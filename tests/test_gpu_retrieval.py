@@ -854,7 +854,7 @@ def _dense_inputs(noise, paired, seed=91, n=1000, d=256, k=160):
 @pytest.mark.gpu
 @pytest.mark.parametrize("noise,seed", [(3e-3, 17), (3e-4, 91)])
 def test_level2_rescore_near_ties(torch_cuda, noise, seed):
-    """The K14 level-2 re-score (fp16 + 8-bit residual planes, bound e8_q + (1 + e8_q) e8_g) at its bound's scale:
+    """The K14 level-2 re-score (fp16 + bf16 residual planes, bound el_q + (1 + el_q) el_g) at its bound's scale:
     160 near-duplicate rows whose pair scores differ by ~1e-6 (3e-3 noise: decided at level 2, some within a few
     bounds) or ~1e-8 (3e-4 noise: inside the level-2 bound, every such pair falls through to fp64; the smallest
     gap between a pair's score and its GT score is still 6.5e-13, far above fp64 summation-order noise, so the
@@ -867,6 +867,34 @@ def test_level2_rescore_near_ties(torch_cuda, noise, seed):
     sess = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64)
     r, cc = sess.run(torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
     assert np.array_equal(r, R.rank_counts(s, t2v)) and np.array_equal(cc, R.rank_counts(s.T, v2t))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [512, 768])
+def test_paired_prep_plane_widths(torch_cuda, d):
+    """The paired fp16 prep writes its fp16 and bf16-residual planes write-through in 16-B pieces, lanes L and L ^ 1
+    swapping halves of two 256-element chunks (an odd last chunk in 8-B pieces): rows of 512 and 768 elements (two
+    and three chunks; 1,024 is the C1 default, 256 the level-3 test's) give the oracle's exact ranks, one evaluation
+    and a batch of two, near-duplicates included so level 2 reads the residual plane."""
+    import torch
+    from cmve import engine
+    c, v, t2v, v2t = _dense_inputs(3e-3, True, seed=23, d=d)
+    n = c.shape[0]
+    s = R.exact_scores64(c, v)
+    er, ec = R.rank_counts(s, t2v), R.rank_counts(s.T, v2t)
+    ct, vt = torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda()
+    sess = engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64)
+    assert sess.paired
+    r, cc = sess.run(ct, vt)
+    assert np.array_equal(r, er) and np.array_equal(cc, ec)
+    sb = [engine.RankSession(n, n, d, row_gts=t2v, col_gts=v2t, dtype=torch.float64) for _ in range(2)]
+    b = engine.RankBatch(sb, [(ct, vt), (ct.clone(), vt.clone())])
+    b.run()
+    torch.cuda.synchronize()
+    for x in sb:
+        h = x.out.cpu().numpy()
+        assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)
+    b.close()
 
 
 @pytest.mark.gpu
