@@ -563,17 +563,26 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
   const int nw = (int)(blockDim.x >> 6);  // waves per block
   const int64_t stride = (int64_t)(gridDim.x / G) * nw;
   int64_t k = 0;
-  for (int64_t c = (int64_t)(blockIdx.x / G) * nw + wave; c < total; c += stride) {
-    if (pre[k + 1] <= c) {  // the bucket holding pair c: binary search of the prefix (the flat walk of
+  auto entry = [&](int64_t cc) -> uint64_t {  // pair cc's entry (cc increases call by call); 0 past the end
+    if (cc >= total) return 0ull;
+    if (pre[k + 1] <= cc) {  // the bucket holding pair cc: binary search of the prefix (the flat walk of
       int64_t lo = k + 1, hi = nk - 1;  // a 256-bucket evaluation would scan up to 256 LDS words)
       while (lo < hi) {
         const int64_t mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= c) lo = mid;
+        if (pre[mid] <= cc) lo = mid;
         else hi = mid - 1;
       }
       k = lo;
     }
-    const uint64_t u = gld(cand + nb + (xcd + G * k) * cap_b + (c - pre[k]));
+    return gld(cand + nb + (xcd + G * k) * cap_b + (cc - pre[k]));
+  };
+  // the next pair's entry is loaded one pair ahead: in flight with this pair's row loads (as a dependent load
+  // at the top of each pair it added a round trip to every pair)
+  const int64_t c0 = (int64_t)(blockIdx.x / G) * nw + wave;
+  uint64_t u_next = entry(c0);
+  for (int64_t c = c0; c < total; c += stride) {
+    const uint64_t u = u_next;
+    u_next = entry(c + stride);
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     uint32_t flags = (uint32_t)(u >> 62);
