@@ -84,6 +84,9 @@ SIGNATURES = {
     "cmve_eval_batch_create": (C.c_int, [C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp,
                                          _vp]),
     "cmve_eval_batch_run": (C.c_int, [_vp, _vp, C.c_int32]),
+    "cmve_eval_batch_run_split": (C.c_int, [_vp, _vp, _vp, C.c_int32]),
+    "cmve_stream_create_cu_mask": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp)]),
+    "cmve_stream_destroy": (C.c_int, [_vp]),
     "cmve_eval_batch_destroy": (C.c_int, [_vp]),
     "cmve_topk_dense_merge": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp]),
     "cmve_mha_absorbed": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _vp, _i64, _f64,
@@ -160,7 +163,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -646,11 +646,13 @@ class RankBatch:
         self.sessions, self.outs, self.stream = sessions, outs, stream
         self._h = stream_handle(s0.device, stream) if stream is not None else None
 
-    def run(self, timing_slot: int = -1, wait_current: bool = True):
+    def run(self, timing_slot: int = -1, wait_current: bool = True, prep_stream=None):
         """Enqueue the batch; ``timing_slot`` >= 0 records its launches' durations in that slot of the stream
         handle's timing ring (``kernel_timing``).  With a batch stream the run first waits for the work already
         enqueued on the caller's current stream (the producer that refilled the inputs, as RankSession.enqueue
-        does); ``wait_current=False`` skips that for inputs known to be complete."""
+        does); ``wait_current=False`` skips that for inputs known to be complete.  ``prep_stream`` (a torch
+        stream): the prep launch goes there (``cmve_eval_batch_run_split``) -- e.g. a stream on CUs of its own,
+        ``cu_mask_stream``."""
         if not self._b:
             raise RuntimeError("RankBatch.run: the batch was closed")
         if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
@@ -660,7 +662,11 @@ class RankBatch:
             if cur.cuda_stream != self.stream.cuda_stream:
                 self.stream.wait_stream(cur)
         h = self._h if self._h is not None else handle(self.sessions[0].device)
-        check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
+        if prep_stream is not None:
+            check(lib.cmve_eval_batch_run_split(h, self._b, C.c_void_p(prep_stream.cuda_stream), int(timing_slot)),
+                  "cmve_eval_batch_run_split")
+        else:
+            check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
 
     def kernel_timing(self, slot: int):
         """(prep, rank GEMM, 0, finish) durations in ms of the batch run that used `slot` (each launch's own
@@ -871,3 +877,22 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
         out[i] = pi
         p += len(l)
     return out
+
+
+def cu_mask_stream(device, cus):
+    """A torch stream (ExternalStream over a HIP stream of libcmve.so's) whose kernels run only on the CUs in
+    ``cus`` (indices into the device's CUs: ``cmve_stream_create_cu_mask``).  The HIP stream lives as long as the
+    process (streams are few and long-lived)."""
+    import torch
+    dev = torch.device(device)
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (n + 31) // 32
+    mask = (C.c_uint32 * words)()
+    for c in cus:
+        if not 0 <= c < n:
+            raise ValueError(f"cu_mask_stream: CU {c} outside 0..{n - 1}")
+        mask[c // 32] |= 1 << (c % 32)
+    ptr = C.c_void_p()
+    with torch.cuda.device(dev):
+        check(lib.cmve_stream_create_cu_mask(mask, words, C.byref(ptr)), "cmve_stream_create_cu_mask")
+    return torch.cuda.ExternalStream(ptr.value, device=dev)

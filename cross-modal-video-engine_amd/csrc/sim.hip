@@ -21,6 +21,8 @@
 // tile order, which walks 8 gallery tiles x all query tiles.
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "cmve_internal.h"
 
 namespace cmve {
@@ -2239,6 +2241,7 @@ struct cmve_eval_batch {
   bool fix_launch = false;        // the rank GEMM lists its undecided pairs for a fix-up launch
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
+  hipEvent_t ev_in = nullptr, ev_prep = nullptr;  // cmve_eval_batch_run_split's stream hand-offs
 };
 
 // the batch's rank geometry: 128 x 128 tiles (8 waves of 32 x 64, a 3-stage ring of 32 KiB stages, one block of
@@ -2356,9 +2359,9 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
 
 // timing_slot >= 0: the three launches' own start / stop into that slot of h's ring (cmve_eval_kernel_timing:
 // prep, rank GEMM, 0, finish -- durations of the whole batch's launches) and the event spans (cmve_eval_timing)
-extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_slot) {
-  CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
-  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
+// ps: the prep launch's stream (h->stream, or cmve_eval_batch_run_split's prep stream: it first waits for the work
+// enqueued on h->stream, and the rank GEMM waits for the prep)
+static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, int32_t timing_slot) {
   hipEvent_t* ev = nullptr;
   hipEvent_t* kev = nullptr;
   if (timing_slot >= 0) {
@@ -2374,11 +2377,22 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
     if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
   };
   hipStream_t s = h->stream;
-  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
+  const bool split = ps != s;
+  if (split) {
+    if (!b->ev_in) CMVE_HIP(hipEventCreateWithFlags(&b->ev_in, hipEventDisableTiming));
+    if (!b->ev_prep) CMVE_HIP(hipEventCreateWithFlags(&b->ev_prep, hipEventDisableTiming));
+    CMVE_HIP(hipEventRecord(b->ev_in, s));  // (the batch's previous run and whatever the caller enqueued before)
+    CMVE_HIP(hipStreamWaitEvent(ps, b->ev_in, 0));
+  }
+  if (ev) CMVE_HIP(hipEventRecord(ev[0], ps));
   arm(0);
-  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
+  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, ps);
   if (st) return st;
-  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
+  if (ev) CMVE_HIP(hipEventRecord(ev[1], ps));
+  if (split) {
+    CMVE_HIP(hipEventRecord(b->ev_prep, ps));
+    CMVE_HIP(hipStreamWaitEvent(s, b->ev_prep, 0));
+  }
   arm(1);
   switch (b->mode) {
     case CMVE_SIM_F16: st = launch_rank_batch<CMVE_SIM_F16>(b->d_args, b->count, b->nq_pad, b->ng_pad, b->bm, b->bn, s); break;
@@ -2399,8 +2413,38 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   return CMVE_OK;
 }
 
+extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_slot) {
+  CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
+  return eval_batch_run(h, b, h->stream, timing_slot);
+}
+
+extern "C" int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t b, void* prep_stream, int32_t timing_slot) {
+  CMVE_REQUIRE(h && b && b->d_items && b->d_args && prep_stream, "cmve_eval_batch_run_split: NULL argument");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS,
+               "cmve_eval_batch_run_split: bad timing slot");
+  return eval_batch_run(h, b, (hipStream_t)prep_stream, timing_slot);
+}
+
+// a stream whose kernels run only on the CUs set in mask (bit i of word i / 32: CU i), hipExtStreamCreateWithCUMask
+extern "C" int cmve_stream_create_cu_mask(const uint32_t* mask, int32_t nwords, void** stream) {
+  CMVE_REQUIRE(mask && nwords > 0 && stream, "cmve_stream_create_cu_mask: NULL argument");
+  hipStream_t st = nullptr;
+  CMVE_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)nwords, mask));
+  *stream = (void*)st;
+  return CMVE_OK;
+}
+
+extern "C" int cmve_stream_destroy(void* stream) {
+  CMVE_REQUIRE(stream, "cmve_stream_destroy: NULL stream");
+  CMVE_HIP(hipStreamDestroy((hipStream_t)stream));
+  return CMVE_OK;
+}
+
 extern "C" int cmve_eval_batch_destroy(cmve_eval_batch_t b) {
   if (!b) return CMVE_OK;
+  if (b->ev_in) (void)hipEventDestroy(b->ev_in);
+  if (b->ev_prep) (void)hipEventDestroy(b->ev_prep);
   (void)hipFree(b->d_items);
   (void)hipFree(b->d_args);
   delete b;

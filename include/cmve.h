@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 18
+#define CMVE_ABI_VERSION 19
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -446,6 +446,14 @@ int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* co
 /* timing_slot: -1, or a slot of h's timing ring receiving the batch's launch durations (cmve_eval_kernel_timing:
  * prep, rank GEMM, 0, finish; cmve_eval_timing: the event spans), as for cmve_eval_ranks */
 int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch, int32_t timing_slot);
+/* the same run with its prep launch on prep_stream (a hipStream_t): the prep first waits for the work enqueued on
+ * h's stream, the rank GEMM and the finish (on h's stream) wait for the prep.  With the prep stream and the batch
+ * streams on disjoint CU sets (cmve_stream_create_cu_mask) one batch's HBM-bound prep runs beside another's rank
+ * GEMM instead of taking every CU in turn.  Results are those of cmve_eval_batch_run. */
+int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t batch, void* prep_stream, int32_t timing_slot);
+/* a HIP stream restricted to the CUs set in mask (bit i of word i / 32 = CU i; hipExtStreamCreateWithCUMask) */
+int cmve_stream_create_cu_mask(const uint32_t* mask, int32_t nwords, void** stream);
+int cmve_stream_destroy(void* stream);
 int cmve_eval_batch_destroy(cmve_eval_batch_t batch);
 typedef struct cmve_eval_graph* cmve_eval_graph_t;
 int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 18
+    assert _lib.lib.cmve_abi_version() == 19
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)

@@ -870,6 +870,42 @@ def test_level2_rescore_near_ties(torch_cuda, noise, seed):
 
 
 @pytest.mark.gpu
+def test_rank_batch_run_split_streams(golden, torch_cuda):
+    """cmve_eval_batch_run_split: the batch's prep on a stream of its own over half the CUs
+    (cmve_stream_create_cu_mask), the rank GEMM + finish on the batch's stream over the other half: every output
+    word equals the plain run's, run after run (the prep waits for the batch's previous finish)."""
+    import torch
+    from cmve import engine
+    v, c, vid, cid = _c1()
+    v2t_gt, t2v_gt = R.get_gt(vid, cid)
+    rows, cols = [t2v_gt[i] for i in range(len(cid))], v2t_gt
+    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
+    rng = np.random.default_rng(11)
+    sets = [(torch.from_numpy(c if j == 0 else c + 0.3 * rng.standard_normal(c.shape)).cuda(),
+             torch.from_numpy(v).cuda()) for j in range(3)]
+    ref_s = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64) for _ in sets]
+    ref_b = engine.RankBatch(ref_s, sets)
+    ref_b.run()
+    torch.cuda.synchronize()
+    ref = [x.out.clone() for x in ref_s]
+    ref_b.close()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    ps = engine.cu_mask_stream("cuda:0", [k for k in range(n_cu) if k % 2 == 0])
+    gs = engine.cu_mask_stream("cuda:0", [k for k in range(n_cu) if k % 2 == 1])
+    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64, stream=gs) for _ in sets]
+    b = engine.RankBatch(sess, sets, stream=gs)
+    for _ in range(3):
+        b.run(prep_stream=ps)
+    torch.cuda.synchronize()
+    for x, r in zip(sess, ref):
+        assert torch.equal(x.out, r)
+    g = golden("retrieval_c1")
+    h = sess[0].out.cpu().numpy()
+    assert np.array_equal(h[16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[16 + n_q:], g["v2t_ranks"])
+    b.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("d", [512, 768])
 def test_paired_prep_plane_widths(torch_cuda, d):
     """The paired fp16 prep writes its fp16 and bf16-residual planes write-through in 16-B pieces, lanes L and L ^ 1
