@@ -103,8 +103,9 @@ class CAbiComm:
         r0, w0 = _world()
         self.rank = r0 if rank is None else int(rank)
         self.world = w0 if world is None else int(world)
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
-        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.device = torch.device(dev.type, idx)  # indexed: tensors report 'cuda:N', never bare 'cuda'
         if uid is None:
             buf = C.create_string_buffer(_lib.DIST_UNIQUE_ID_BYTES)
             if self.rank == 0:
@@ -151,8 +152,10 @@ class CAbiComm:
         Work -- the stream order already holds every later reader)."""
         x = x.contiguous()
         code = self._code(x)
-        if out.dtype != x.dtype or out.numel() != self.world * x.numel() or not out.is_contiguous():
-            raise ValueError("CAbiComm.all_gather_into: out must be world x the input, same dtype, contiguous")
+        if (out.dtype != x.dtype or out.numel() != self.world * x.numel() or not out.is_contiguous()
+                or out.device != self.device):
+            raise ValueError(f"CAbiComm.all_gather_into: out must be world x the input, same dtype, contiguous, on "
+                             f"{self.device}")
         self._on_current()
         _lib.check(_lib.lib.cmve_dist_allgather(self._h, engine._ptr(x), x.numel(), code, engine._ptr(out)),
                    "cmve_dist_allgather")

@@ -681,6 +681,7 @@ class RankBatch:
             lib.cmve_eval_batch_destroy(self._b)
             self._b = None
 
+
     def __del__(self):
         try:
             self.close()
@@ -881,11 +882,16 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
 
 def cu_mask_stream(device, cus):
     """A torch stream (ExternalStream over a HIP stream of libcmve.so's) whose kernels run only on the CUs in
-    ``cus`` (indices into the device's CUs: ``cmve_stream_create_cu_mask``).  The HIP stream lives as long as the
-    process (streams are few and long-lived)."""
+    ``cus`` (indices into the device's CUs, at least one: ``cmve_stream_create_cu_mask``).  The HIP stream is
+    destroyed (``cmve_stream_destroy``) when the returned object is garbage-collected or passed to
+    ``close_cu_mask_stream``, whichever comes first; synchronise it before dropping it."""
+    import weakref
     import torch
     dev = torch.device(device)
     n = torch.cuda.get_device_properties(dev).multi_processor_count
+    cus = list(cus)
+    if not cus:  # an all-zero mask: the runtime rejects the stream's kernels or never schedules them
+        raise ValueError("cu_mask_stream: no CU given")
     words = (n + 31) // 32
     mask = (C.c_uint32 * words)()
     for c in cus:
@@ -895,4 +901,20 @@ def cu_mask_stream(device, cus):
     ptr = C.c_void_p()
     with torch.cuda.device(dev):
         check(lib.cmve_stream_create_cu_mask(mask, words, C.byref(ptr)), "cmve_stream_create_cu_mask")
-    return torch.cuda.ExternalStream(ptr.value, device=dev)
+    st = torch.cuda.ExternalStream(ptr.value, device=dev)
+    fin = weakref.finalize(st, lib.cmve_stream_destroy, C.c_void_p(ptr.value))
+    fin.atexit = False  # (at interpreter exit the HIP runtime may already be torn down: the process releases it)
+    _CU_STREAMS[ptr.value] = fin
+    return st
+
+
+_CU_STREAMS = {}
+
+
+def close_cu_mask_stream(stream):
+    """Destroy a ``cu_mask_stream`` now (after synchronising it); later uses of the object are errors."""
+    fin = _CU_STREAMS.pop(stream.cuda_stream, None)
+    if fin is None:
+        raise ValueError("close_cu_mask_stream: not a live cu_mask_stream")
+    stream.synchronize()
+    fin()

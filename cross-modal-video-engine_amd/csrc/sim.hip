@@ -2318,6 +2318,15 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
                        g[i]->n_pad == g[0]->n_pad && q[i]->d == q[0]->d && q[i]->d_pad == q[0]->d_pad &&
                        P.qf == P0.qf && P.gf == P0.gf && P.paired == P0.paired,
                    "cmve_eval_batch_create: evaluation %d differs in shape / dtype / pairing from the first", i);
+      // the batch's launches pick their kernels (the specialised paired prep, the level-2 re-score, a fix-up launch)
+      // from the first evaluation's plan: every evaluation must plan the same way -- e.g. a row-strided input whose
+      // rows are not 16-B aligned takes no register prep and no residual plane, which the specialised prep would
+      // still read and write through
+      CMVE_REQUIRE(P.sq.vec == P0.sq.vec && P.sg.vec == P0.sg.vec && (P.sq.lo16 != nullptr) == (P0.sq.lo16 != nullptr) &&
+                       (P.sg.lo16 != nullptr) == (P0.sg.lo16 != nullptr) && P.fix_launch == P0.fix_launch &&
+                       (P.c.l3_count != nullptr) == (P0.c.l3_count != nullptr),
+                   "cmve_eval_batch_create: evaluation %d's inputs take another path than the first's (row alignment "
+                   "or stride: every evaluation of a batch needs 16-B aligned rows if the first has them)", i);
       for (int j = 0; j < i; ++j)
         CMVE_REQUIRE(ws[j] != ws[i] && out[j] != out[i],
                      "cmve_eval_batch_create: evaluations %d and %d share a workspace or an output", j, i);

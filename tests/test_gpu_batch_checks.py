@@ -1,0 +1,83 @@
+"""GPU checks of the K14 batch's argument planning (cmve_eval_batch_create) and of the CMVE_EVAL_PAIRED safety path,
+through the C ABI: inputs a batch cannot run with the first evaluation's kernels are refused, and lists that are not
+the asserted one-to-one pairing are counted (out[11]) instead of writing out of range.  The ranks of the sessions
+involved equal the oracle's (oracle/retrieval.py, pinned to LINAS-engine/util/metrics.py:124-157 via
+retrieval_c1.npz)."""
+import numpy as np
+import pytest
+
+import synth
+from oracle import retrieval as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _c1_lists():
+    v, c, vid, cid = synth.c1_embeddings()
+    v2t_gt, t2v_gt = R.get_gt(vid, cid)
+    return v, c, [t2v_gt[i] for i in range(len(cid))], v2t_gt
+
+
+@pytest.mark.parametrize("paired", [True, False])
+def test_rank_batch_refuses_unaligned_later_input(torch_cuda, paired):
+    """cmve_eval_batch_create takes every launch's kernels from the first evaluation's plan: a later evaluation whose
+    rows are not 16-B aligned (a column slice of a wider buffer) would plan without the residual plane (and, paired,
+    without the paired prep), so the batch refuses it -- and that session alone still ranks as the oracle does."""
+    torch = torch_cuda
+    from cmve import engine
+    v, c, rows, cols = _c1_lists()
+    if not paired:  # multi-GT v2t lists: the general prep, which plans the residual plane from the rows' alignment
+        cols = [list(l) + [(j + 1) % len(cols)] if j % 3 == 0 else list(l) for j, l in enumerate(cols)]
+    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
+    good = (torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    wide_c = torch.zeros((n_q, d + 2), dtype=torch.float64, device="cuda")
+    wide_c[:, 1:1 + d] = good[0]
+    sliced = wide_c[:, 1:1 + d]  # rows 8-B aligned only, stride(1) == 1
+    assert sliced.stride(1) == 1 and (sliced.data_ptr() % 16) != 0
+    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64) for _ in range(2)]
+    with pytest.raises(RuntimeError, match="another path|differs in shape / dtype / pairing"):
+        engine.RankBatch(sess, [good, (sliced, good[1])])
+    t2v, v2t = sess[1].run(sliced, good[1])
+    s = R.exact_scores64(c, v)
+    assert np.array_equal(t2v, R.rank_counts(s, rows)) and np.array_equal(v2t, R.rank_counts(s.T, cols))
+
+
+def test_paired_flag_with_lists_that_are_no_pairing(torch_cuda):
+    """CMVE_EVAL_PAIRED asserts a one-to-one pairing; the paired prep checks the t2v side per caption and counts the
+    captions that break it in out[11] (a caption with no GT, with two GTs, with a video id past the gallery) without
+    writing outside the workspace.  RankSession.run raises on it; a batch reports the same count per evaluation."""
+    torch = torch_cuda
+    from cmve import engine
+    v, c, rows, cols = _c1_lists()
+    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
+    x = (torch.from_numpy(c).cuda(), torch.from_numpy(v).cuda())
+    bad = [list(l) for l in rows]
+    bad[0] = []                  # no GT
+    bad[1] = [bad[1][0], 7]      # two GTs
+    bad[2] = [n_g + 5]           # a video id past the gallery
+    bad_csr = engine.csr(bad, torch.device("cuda", 0))
+
+    def broken():
+        s = engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64)
+        assert s.paired
+        s.row = bad_csr  # what a C caller passing CMVE_EVAL_PAIRED with these lists hands the library
+        s._args = None
+        return s
+
+    s = broken()
+    with pytest.raises(RuntimeError, match="one-to-one"):
+        s.run(*x)
+    assert int(s.host[11]) == 3
+    sess = [broken() for _ in range(2)]
+    b = engine.RankBatch(sess, [x, x])
+    b.run()
+    torch.cuda.synchronize()
+    assert [int(t.out[11]) for t in sess] == [3, 3]
+    b.close()
