@@ -267,7 +267,13 @@ constexpr size_t stage_bytes() {
 // loop (G128) or the phased G256 schedule
 template <int BM, int BN, bool PHASED, int NW = 4>
 constexpr bool is_ring() {
-  return !PHASED && (BN == 64 || (BM == 128 && BN == 128 && NW == 8)) && (BM == 64 || BM == 128);
+  return !PHASED && (((BN == 64 || (BM == 128 && BN == 128 && NW == 8)) && (BM == 64 || BM == 128)) ||
+                     (BM == 256 && BN == 128 && NW == 8));
+}
+// the K14 batches' 256 x 128 tiles (one block of 8 waves of 64 x 64 per CU, up to 256 VGPRs)
+template <int BM, int BN>
+constexpr bool is_big_ring() {
+  return BM == 256 && BN == 128;
 }
 
 // staging ring depth of the 2-stage (non-phased) loop: the G64 tiles of small problems keep NS - 1
@@ -290,6 +296,10 @@ constexpr int ring_stages() {
 #define CMVE_G128R_STAGES 2
 #endif
   // (64 x 64, 128 x 64 and the 8-wave 128 x 128; the 4-wave G128 of mid-size problems keeps its 2-stage loop)
+#ifndef CMVE_G256R_STAGES
+#define CMVE_G256R_STAGES 3
+#endif
+  if (!PHASED && is_big_ring<BM, BN>() && NW == 8) return CMVE_G256R_STAGES;  // (3 x 48 KiB: one block per CU)
   return (PHASED || (BN != 64 && !(BM == 128 && BN == 128 && NW == 8)) || (BM != 64 && BM != 128))
              ? 2
              : (BM == 64 ? CMVE_G64_STAGES : CMVE_G128R_STAGES);
@@ -357,6 +367,9 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_L2_P
 #define CMVE_L2_P 1  // K14 level-2 re-score: pairs per wave in flight at once (2: 128+ VGPRs, spills at 4 waves per SIMD)
 #endif
+#ifndef CMVE_L2_P_BIG
+#define CMVE_L2_P_BIG 2  // the same for the batches' 256 x 128 tiles (one 8-wave block per CU: registers to spare)
+#endif
 #ifndef CMVE_L2_P_ONE
 #define CMVE_L2_P_ONE 2  // the same for one evaluation's G64 rank GEMM (4 waves, ~6 listed pairs per tile: one round)
 #endif
@@ -366,7 +379,8 @@ struct EpiLds<BM, BN, false, INL> {
 #define CMVE_BATCH_WPE 4  // the batch ring kernels: waves per SIMD the register budget must allow (<= 128 VGPRs)
 #endif
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
-__global__ __launch_bounds__(WM * WN * 64, BATCH ? CMVE_BATCH_WPE : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2))
+__global__ __launch_bounds__(WM * WN * 64, BATCH ? (is_big_ring<WM * TM * 16, WN * 64>() ? 2 : CMVE_BATCH_WPE)
+                                                 : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2))
 void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
   // a batch's blocks: the (evaluation, tile) pairs in evaluation-major order, cut into 8 contiguous ranges, one per
@@ -865,7 +879,7 @@ void sim_kernel(
               // direction left undecided goes to the level-3 list (fp64 in the finish launch, off this kernel's
               // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
               // entries: no other wave touches them)
-              constexpr int RP = BATCH ? CMVE_L2_P : CMVE_L2_P_ONE;
+              constexpr int RP = BATCH ? (is_big_ring<BM, BN>() ? CMVE_L2_P_BIG : CMVE_L2_P) : CMVE_L2_P_ONE;
               for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
                 int64_t qr[RP], gc[RP];
                 uint32_t ent[RP];
@@ -2257,9 +2271,16 @@ static int batch_geo_force() {
   }();
   return force;
 }
-static int batch_geo_bm(int64_t nq_pad) { return (batch_geo_force() != 64 && nq_pad % 128 == 0) ? 128 : 64; }
+static bool batch_geo_big(int64_t nq_pad, int64_t ng_pad, int mode) {
+  return batch_geo_force() == 256128 && nq_pad % 256 == 0 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3;
+}
+static int batch_geo_bm(int64_t nq_pad, int64_t ng_pad, int mode) {
+  if (batch_geo_big(nq_pad, ng_pad, mode)) return 256;
+  return (batch_geo_force() != 64 && nq_pad % 128 == 0) ? 128 : 64;
+}
 static int batch_geo_bn(int64_t nq_pad, int64_t ng_pad, int mode) {
   const int f = batch_geo_force();
+  if (batch_geo_big(nq_pad, ng_pad, mode)) return 128;
   return (f != 64 && f != 12864 && nq_pad % 128 == 0 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3) ? 128 : 64;
 }
 
@@ -2280,8 +2301,10 @@ static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int6
 template <int MODE>
 static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
                              int bm, int bn, hipStream_t stream) {
-  if constexpr (MODE != CMVE_SIM_BF16X3)
+  if constexpr (MODE != CMVE_SIM_BF16X3) {
+    if (bm == 256 && bn == 128) return launch_rank_batch<MODE, 2, 4>(tab, count, nq_pad, ng_pad, stream);
     if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
+  }
   return bm == 128 ? launch_rank_batch<MODE, 1, 2>(tab, count, nq_pad, ng_pad, stream)
                    : launch_rank_batch<MODE, 1, 1>(tab, count, nq_pad, ng_pad, stream);
 }
@@ -2306,7 +2329,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
                                "128^2, e.g. 1,000 x 1,000) with the inline fix-up");
     if (P.c.stamps) {  // kernel studies (CMVE_EVAL_DBG & 128): the first evaluation's prep / finish blocks, and
                        // every evaluation's rank tiles while the stamp buffer's 1,024 tile slots last
-      const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad)) *
+      const int64_t per = (q[i]->n_pad / batch_geo_bm(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff)) *
                           (g[i]->n_pad / batch_geo_bn(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff));
       P.a.dbg_stamps = (i + 1) * per <= 1024 ? P.c.stamps + 3 * 1024 * 8 + (size_t)i * per * 8 : nullptr;
       if (i > 0) P.c.stamps = nullptr;
@@ -2333,7 +2356,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
     }
     items[(size_t)i] = cmve::EvalItem{P.sq, P.sg, P.c};
     // (launch_geo fills these for a single launch)
-    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad),
+    geo_fill(P.a, q[i]->n_pad, g[i]->n_pad, batch_geo_bm(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff),
              batch_geo_bn(q[i]->n_pad, g[i]->n_pad, mode_flags & 0xff));
     args[(size_t)i] = P.a;
   }
@@ -2345,7 +2368,7 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->paired = P0.paired;
   b->nq_pad = q[0]->n_pad;
   b->ng_pad = g[0]->n_pad;
-  b->bm = batch_geo_bm(b->nq_pad);
+  b->bm = batch_geo_bm(b->nq_pad, b->ng_pad, b->mode);
   b->bn = batch_geo_bn(b->nq_pad, b->ng_pad, b->mode);
   b->sq0 = P0.sq;
   b->sg0 = P0.sg;

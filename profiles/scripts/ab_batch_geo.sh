@@ -1,7 +1,7 @@
 #!/bin/bash
 # K14 batches: the batch rank GEMM's geometries (CMVE_BATCH_GEO = 64: 64 x 64, default: 128 x 64, 128128: the
 # 8-wave 128 x 128), alternating; the batch tests first under each
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out || exit 1
 GEOS=${GEOS:-"64 128 128128"}
 for g in $GEOS; do

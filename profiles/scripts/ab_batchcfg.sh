@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: the headline over batch sizes / streams in flight (the kernels changed since round 3's sweep)
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/bcfg || exit 1
 A="--steps 20 --warmup 5 --no-shard-leg --no-extras --no-cpu-baseline --no-replay"
 for r in 1 2; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 A/B of environment / library variants of the headline on one box: AB_VARS="name|ENV=1 ENV2=0|lib ..." (lib
 # optional, relative to the repo); prints the headline (3 / 1 streams) and the batch's isolated launch durations
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/ab || exit 1
 A="--steps 20 --warmup 5 --no-shard-leg --no-extras --no-cpu-baseline --no-replay ${AB_ARGS:-}"
 for r in 1 2; do

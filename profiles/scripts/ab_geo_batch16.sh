@@ -1,6 +1,6 @@
 #!/bin/bash
 # K14 batches: rank-GEMM geometry x batch size, alternating (CMVE_BATCH_GEO: default 128 x 64, 128128 = 8-wave 128 x 128)
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out || exit 1
 A="--steps 20 --warmup 5 --no-shard-leg --no-extras --no-cpu-baseline --no-c3-sharded --no-c5"
 V=${GEO_VARIANTS:-"b10::--batch=10 g128b10:CMVE_BATCH_GEO=128128:--batch=10"}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: C4 end to end (30,364 queries, no per-batch loop) for mha_absorbed variants: CMVE_MHA_HPW x CMVE_MHA_ROWS
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/abm || exit 1
 for v in ${MHA_VARS:-"4 1" "2 1" "2 2" "2 4" "4 2"}; do
   set -- $v

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: the headline with the batches' preps on their own CUs (--cu-split N) vs every launch on every CU
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/split || exit 1
 A="--steps 20 --warmup 5 --no-shard-leg --no-extras --no-cpu-baseline --no-replay"
 for r in 1 2; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # C4 at its configured size under one FETCH_SIZE pass: the fix-up / rank GEMM / attention kernels' fetched bytes
 # (2 x FETCH_SIZE: the gfx950 half-count) and durations, last launches of each
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 mkdir -p "$R/gpurun_out/fxp" || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$R/gpurun_out/fxp/fetch" -o run -- python3 "$R/tools/fusion_bench.py" --loop-q 0 --sample 16 > "$R/gpurun_out/fxp/fetch.log" 2>&1 || { tail -5 "$R/gpurun_out/fxp/fetch.log"; exit 1; }

@@ -2,7 +2,7 @@
 # rocprofv3 counter calibration (run on the GPU box via gpurun): tools/calib.py's known-byte launches under a
 # FETCH_SIZE pass and a WRITE_SIZE pass (each with --kernel-trace only), reduced by tools/calib_reduce.py.
 set -euo pipefail
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 OUT=$R/gpurun_out/calib
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 #!/bin/bash
 # C4 at its configured size (30,364 queries x 44,493 videos): fusion_bench without the per-batch loop, plain and
 # under a rocprofv3 kernel trace -> gpurun_out/<TAG>/{fb.json, trace/}
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=${1:-c4}
 cd "$R" && mkdir -p gpurun_out/$TAG || exit 1
 O=$R/gpurun_out/$TAG

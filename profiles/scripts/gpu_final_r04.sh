@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4 final tree: every -m gpu test, smoke(), and the default bench line -> gpurun_out/final/
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/final || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/final/gpu_tests.txt 2>&1
 rc=$?; tail -2 gpurun_out/final/gpu_tests.txt; [ $rc -ne 0 ] && exit $rc

@@ -1,11 +1,11 @@
 #!/bin/bash
 # round 4, first box: counter calibration, the headline with the streams on distinct input groups (3 and 1
 # in flight), and a one-stream trace + FETCH / WRITE passes of the batch launches
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd "$R" && mkdir -p gpurun_out/r04a || exit 1
 O=gpurun_out/r04a
 HB="--no-shard-leg --no-extras --no-cpu-baseline"
-timeout -k 10 300 bash tools/calib.sh > $O/calib.log 2>&1 || { echo "calib failed"; tail -20 $O/calib.log; exit 1; }
+timeout -k 10 300 bash profiles/scripts/calib.sh > $O/calib.log 2>&1 || { echo "calib failed"; tail -20 $O/calib.log; exit 1; }
 cat $O/calib.log
 timeout -k 10 300 python bench.py $HB > $O/bench3.log 2>&1 || { echo "bench3 failed"; tail -20 $O/bench3.log; exit 1; }
 timeout -k 10 300 python bench.py $HB --inflight 1 > $O/bench1.log 2>&1 || { echo "bench1 failed"; tail -20 $O/bench1.log; exit 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 iteration box: the eval parity tests, the headline at 3 / 1 streams, and a one-stream trace + FETCH /
 # WRITE passes of the timed loop's batch launches (no single-set replay) -> profiles/<TAG>_1ka_*
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 TAG=${1:-r04b}
 cd "$R" && mkdir -p gpurun_out/$TAG || exit 1
 O=gpurun_out/$TAG

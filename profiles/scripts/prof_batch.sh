@@ -1,6 +1,6 @@
 #!/bin/bash
 # K14 batches: kernel trace (one stream: isolated kernel durations) + an L2 counter pass of the same loop
-R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
 cd /tmp && export TMPDIR=/tmp && cd "$R" && mkdir -p gpurun_out || exit 1
 T=${TAG:-b}
 ARGS="--steps 20 --warmup 5 --no-shard-leg --no-extras --no-cpu-baseline --no-c3-sharded --no-c5 ${BATCH_ARGS:---batch 10 --inflight 1}"
