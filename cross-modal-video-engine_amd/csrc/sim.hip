@@ -155,26 +155,37 @@ __device__ __forceinline__ void tile_grouped(int L, int nblk_m, int nblk_n, int 
   bn = group * GN + (within - bm * gn);
 }
 
-// issue this wave's share of one ROWS x 64 (bf16/fp16) plane: ROWS/8 wave-instructions of 1 KiB
-template <int ROWS, int NW>
+// the LDS image of a staged K-tile of KB (64 or 32) bf16/fp16 columns: row r at r * 2KB bytes, its 16-B chunk k in
+// slot k ^ swz(r) -- conflict-free ds_read_b128 fragment reads (16 rows x one chunk per 16 lanes): 128-B rows
+// (KB = 64, 8 chunks) XOR the row's low 3 bits; 64-B rows (KB = 32, 4 chunks, four rows per 256-B bank line) XOR
+// bits 2-3, so rows r, r + 4, r + 8, r + 12 of one bank offset take four different slots
+template <int KB>
+__device__ __forceinline__ int lds_swz(int r) {
+  return KB == 64 ? (r & 7) : ((r >> 2) & 3);
+}
+
+// issue this wave's share of one ROWS x KB (bf16/fp16) plane: ROWS x 2KB / 1 KiB wave-instructions of 1 KiB
+template <int ROWS, int NW, int KB = BK>
 __device__ __forceinline__ void stage_plane(const uint16_t* __restrict__ src, int64_t ldk, int row0, int k0,
                                             char* lds_plane, int wave, int lane) {
-  constexpr int PER_WAVE = ROWS / 8 / NW;
-  static_assert(PER_WAVE * 8 * NW == ROWS, "plane rows must split evenly over the waves");
+  constexpr int CPR = KB / 8;    // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;  // rows per wave-instruction
+  constexpr int PER_WAVE = ROWS / RPI / NW;
+  static_assert(PER_WAVE * RPI * NW == ROWS, "plane rows must split evenly over the waves");
 #pragma unroll
   for (int it = 0; it < PER_WAVE; ++it) {
     const int chunk = wave * PER_WAVE + it;
-    const int r = chunk * 8 + (lane >> 3);
-    const int c = lane & 7;
-    const int gc = c ^ (r & 7);
+    const int r = chunk * RPI + lane / CPR;
+    const int c = lane % CPR;
+    const int gc = c ^ lds_swz<KB>(r);
     const uint16_t* g = src + (int64_t)(row0 + r) * ldk + k0 + gc * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (lds_void_t*)(lds_plane + chunk * 1024), 16, 0, 0);
   }
 }
 
+template <int KB = BK>
 __device__ __forceinline__ s16x8_t read_frag(const char* plane, int row, int chunk) {
-  // row & 7 == lane & 7 for every fragment row this kernel reads
-  return *(const s16x8_t*)(plane + row * 128 + ((chunk ^ (row & 7)) << 4));
+  return *(const s16x8_t*)(plane + row * (KB * 2) + ((chunk ^ lds_swz<KB>(row)) << 4));
 }
 
 // LDS atomic add in inline asm: the compiler drains vmcnt before any LDS write it emits while
@@ -258,9 +269,9 @@ struct Geo {
 
 // staged bytes per K-tile: one plane per operand; the 2-stage G128 loop stages both planes of a
 // split-bf16 operand per K-tile, the phased G256 loop walks the planes along K (plane_of)
-template <int MODE, int BM, int BN, bool PHASED>
+template <int MODE, int BM, int BN, bool PHASED, int KB = BK>
 constexpr size_t stage_bytes() {
-  return (size_t)((MODE == CMVE_SIM_BF16X3 && !PHASED) ? 2 : 1) * (BM + BN) * BK * 2;
+  return (size_t)((MODE == CMVE_SIM_BF16X3 && !PHASED) ? 2 : 1) * (BM + BN) * KB * 2;
 }
 
 // the ring loop's geometries (G64, 128 x 64 and the 8-wave 128 x 128 of the batches); the others take the 2-stage
@@ -274,6 +285,17 @@ constexpr bool is_ring() {
 template <int BM, int BN>
 constexpr bool is_big_ring() {
   return BM == 256 && BN == 128;
+}
+
+// K-tile depth of a ring geometry's stages: the batches' 8-wave 128 x 128 ring stages 32-deep K-tiles
+// (CMVE_BATCH_KB): at the same LDS, twice as many stages -- three K-tiles in flight instead of one, for a main loop
+// that waits on L2 / Infinity-Cache latency (the stamps: 0.95 us per 64-deep K-tile against ~0.3 us of MFMAs)
+#ifndef CMVE_BATCH_KB
+#define CMVE_BATCH_KB 64
+#endif
+template <int BM, int BN, bool PHASED, int NW>
+constexpr int ring_kb() {
+  return (!PHASED && BM == 128 && BN == 128 && NW == 8) ? CMVE_BATCH_KB : BK;
 }
 
 // staging ring depth of the 2-stage (non-phased) loop: the G64 tiles of small problems keep NS - 1
@@ -300,9 +322,17 @@ constexpr int ring_stages() {
 #define CMVE_G256R_STAGES 3
 #endif
   if (!PHASED && is_big_ring<BM, BN>() && NW == 8) return CMVE_G256R_STAGES;  // (3 x 48 KiB: one block per CU)
+  // the batches' 128 x 128: CMVE_G128R_STAGES x 64-deep K-tiles of LDS, as twice as many 32-deep stages with
+  // CMVE_BATCH_KB = 32 (ring_kb)
   return (PHASED || (BN != 64 && !(BM == 128 && BN == 128 && NW == 8)) || (BM != 64 && BM != 128))
              ? 2
-             : (BM == 64 ? CMVE_G64_STAGES : CMVE_G128R_STAGES);
+             : (BM == 64 ? CMVE_G64_STAGES : CMVE_G128R_STAGES * (BK / ring_kb<BM, BN, PHASED, NW>()));
+}
+
+// LDS of the staging buffers of a non-persistent geometry (the launchers' dynamic shared memory)
+template <int MODE, int BM, int BN, bool PHASED, int NW>
+constexpr size_t ring_lds_bytes() {
+  return ring_stages<MODE, BM, BN, PHASED, NW>() * stage_bytes<MODE, BM, BN, PHASED, ring_kb<BM, BN, PHASED, NW>()>();
 }
 
 #ifdef CMVE_DBG_STAMPS  // diagnostic build only: per-block s_memtime stamps into the (unused) candidate list
@@ -379,7 +409,7 @@ struct EpiLds<BM, BN, false, INL> {
 #define CMVE_BATCH_WPE 4  // the batch ring kernels: waves per SIMD the register budget must allow (<= 128 VGPRs)
 #endif
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
-__global__ __launch_bounds__(WM * WN * 64, BATCH ? (is_big_ring<WM * TM * 16, WN * 64>() ? 2 : CMVE_BATCH_WPE)
+__global__ __launch_bounds__(WM * WN * 64, BATCH ? ((is_big_ring<WM * TM * 16, WN * 64>() || WM * WN == 4) ? 2 : CMVE_BATCH_WPE)
                                                  : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2))
 void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
@@ -397,9 +427,10 @@ void sim_kernel(
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED>();
+  constexpr int KB = ring_kb<BM, BN, PHASED, NW>();  // K-tile depth of the staging buffers (BK but the batch ring)
+  constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED, KB>();
   constexpr int NS = ring_stages<MODE, BM, BN, PHASED, NW>();
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int A_BYTES = BM * KB * 2, B_BYTES = BN * KB * 2;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
@@ -426,7 +457,8 @@ void sim_kernel(
 #endif
 
   // the G64 ring rank kernel re-scores its undecided pairs itself when the K14 host asks (SimArgs::fix_inline)
-  constexpr bool RING = is_ring<BM, BN, PHASED, NW>();
+  // (the batches' default 128 x 128 tiles on 4 waves of 64 x 64 take the ring loop too)
+  constexpr bool RING = is_ring<BM, BN, PHASED, NW>() || (BATCH && BM == 128 && BN == 128 && NW == 4);
   constexpr bool INL = EPI == EPI_RANK && RING;
   __shared__ EpiLds<BM, BN, epi_thr(EPI), INL> epi;
   double sgt_pub = 0.0;  // INL: this thread's row / column GT score (tid < BM + BN), published with the thresholds
@@ -506,12 +538,12 @@ void sim_kernel(
     return;
 #endif
     char* base = smem + s * STAGE_BYTES;
-    const int k0 = t * BK;
-    stage_plane<BM, NW>(a.qhi, a.ldk, m0, k0, base, wave, lane);
-    stage_plane<BN, NW>(a.ghi, a.ldk, n0, k0, base + A_BYTES, wave, lane);
+    const int k0 = t * KB;
+    stage_plane<BM, NW, KB>(a.qhi, a.ldk, m0, k0, base, wave, lane);
+    stage_plane<BN, NW, KB>(a.ghi, a.ldk, n0, k0, base + A_BYTES, wave, lane);
     if (MODE == CMVE_SIM_BF16X3) {
-      stage_plane<BM, NW>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, wave, lane);
-      stage_plane<BN, NW>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, wave, lane);
+      stage_plane<BM, NW, KB>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, wave, lane);
+      stage_plane<BN, NW, KB>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, wave, lane);
     }
   };
 
@@ -879,7 +911,7 @@ void sim_kernel(
               // direction left undecided goes to the level-3 list (fp64 in the finish launch, off this kernel's
               // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
               // entries: no other wave touches them)
-              constexpr int RP = BATCH ? (is_big_ring<BM, BN>() ? CMVE_L2_P_BIG : CMVE_L2_P) : CMVE_L2_P_ONE;
+              constexpr int RP = BATCH ? ((is_big_ring<BM, BN>() || NW == 4) ? CMVE_L2_P_BIG : CMVE_L2_P) : CMVE_L2_P_ONE;
               for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
                 int64_t qr[RP], gc[RP];
                 uint32_t ent[RP];
@@ -1304,9 +1336,16 @@ void sim_kernel(
 #undef CMVE_BAR
   } else if constexpr (RING) {
   // ---- ring of NS stages (G64): K-tiles t+1 .. t+NS-2 stay in flight while K-tile t is consumed ----
-  constexpr int LPS = (BM / 8 / NW + BN / 8 / NW) * (MODE == CMVE_SIM_BF16X3 ? 2 : 1);  // loads / stage / wave
+  constexpr int RPI = 64 / (KB / 8);  // rows per staging wave-instruction (1 KiB)
+  constexpr int LPS = (BM / RPI / NW + BN / RPI / NW) * (MODE == CMVE_SIM_BF16X3 ? 2 : 1);  // loads / stage / wave
+  constexpr int KS = KB / 32;  // 32-deep MFMA steps per K-tile
+#ifndef CMVE_RING_KSPLIT
+#define CMVE_RING_KSPLIT 0
+#endif
+  // the batch rings with CMVE_RING_KSPLIT: fragments and MFMAs one 32-deep step at a time
+  constexpr bool KSPLIT = CMVE_RING_KSPLIT && BATCH && MODE != CMVE_SIM_BF16X3 && KS > 1;
   static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
-  const int nk0 = a.nk0;
+  const int nk0 = a.nk0 * (BK / KB);  // (a.nk0: 64-deep K-tiles; d_pad % 64 == 0)
   // K14: the other set's err_max shards as VECTOR loads, one shard per lane, issued before the first
   // K-tiles (the oldest loads: retired by the first ring wait) and folded after the main loop -- as scalar
   // loads their round trip held the prologue (~2.5 us to the first K-tile in the stamps)
@@ -1352,46 +1391,63 @@ void sim_kernel(
     const char* base = smem + (t % NS) * STAGE_BYTES;
     const char* pA = base;
     const char* pB = base + A_BYTES;
-    s16x8_t fa[2][TM], fb[2][TN];
+    if constexpr (KSPLIT) {
+      // one 32-deep step at a time: its fragments, then its MFMAs (half the fragment registers live)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+        s16x8_t fa1[TM], fb1[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb1[j] = read_frag<KB>(pB, wc * (TN * 16) + j * 16 + frow, chunk);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa1[i] = read_frag<KB>(pA, wr * (TM * 16) + i * 16 + frow, chunk);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa1[i], fb1[j], acc[i][j]);
+      }
+      continue;
+    }
+    s16x8_t fa[KS][TM], fb[KS][TN];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[ks][j] = read_frag(pB, wc * (TN * 16) + j * 16 + frow, chunk);
+      for (int j = 0; j < TN; ++j) fb[ks][j] = read_frag<KB>(pB, wc * (TN * 16) + j * 16 + frow, chunk);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag(pA, wr * (TM * 16) + i * 16 + frow, chunk);
+      for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag<KB>(pA, wr * (TM * 16) + i * 16 + frow, chunk);
     }
     if constexpr (MODE == CMVE_SIM_BF16X3) {  // pairs (lo, hi) then (hi, lo): plane_of's order
       const char* pAl = base + A_BYTES + B_BYTES;
       const char* pBl = base + 2 * A_BYTES + B_BYTES;
-      s16x8_t lx[2][TM > TN ? TM : TN];
+      s16x8_t lx[KS][TM > TN ? TM : TN];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) lx[ks][i] = read_frag(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
+        for (int i = 0; i < TM; ++i) lx[ks][i] = read_frag<KB>(pAl, wr * (TM * 16) + i * 16 + frow, chunk);
       }
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(lx[ks][i], fb[ks][j], acc[i][j]);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) lx[ks][j] = read_frag(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
+        for (int j = 0; j < TN; ++j) lx[ks][j] = read_frag<KB>(pBl, wc * (TN * 16) + j * 16 + frow, chunk);
       }
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], lx[ks][j], acc[i][j]);
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1510,8 +1566,7 @@ static void geo_fill(SimArgs& a, int64_t nq_pad, int64_t ng_pad, int bm, int bn)
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = ring_stages<MODE, G::BM, G::BN, PHASED, G::NW>() *
-                     stage_bytes<MODE, G::BM, G::BN, PHASED>();  // + the static epilogue scratch (EpiLds)
+  const size_t lds = ring_lds_bytes<MODE, G::BM, G::BN, PHASED, G::NW>();  // + the static epilogue scratch (EpiLds)
   // once per instantiation; function-local static init is thread-safe (one host thread per shard / GPU)
   static const hipError_t attr_err = hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2258,12 +2313,13 @@ struct cmve_eval_batch {
   hipEvent_t ev_in = nullptr, ev_prep = nullptr;  // cmve_eval_batch_run_split's stream hand-offs
 };
 
-// the batch's rank geometry: 128 x 128 tiles (8 waves of 32 x 64, a 3-stage ring of 32 KiB stages, one block of
-// 105 KiB per CU) -- a batch has tiles enough to fill the chip with a quarter as many as 64 x 64, and each tile's
-// fixed costs (thresholds, the re-score round trip, the flush) and its L2 -> LDS bytes per MFMA shrink with it;
-// the 55 KiB of LDS and the registers it leaves let another stream's prep blocks share the CU (128 x 64, two
-// 4-wave blocks per CU, filled the LDS: 9.7e10 vs 1.12e11 pairs/s at three streams).  Split-bf16 (whose ring
-// holds both planes) takes 128 x 64; CMVE_BATCH_GEO = 64 / 12864 force 64 x 64 / 128 x 64 (kernel studies).
+// the batch's rank geometry: 128 x 128 tiles on 4 waves of 64 x 64 (a 2-stage ring of 32 KiB stages, two blocks of
+// ~73 KiB per CU, up to 256 VGPRs).  A batch's launch runs beside the other streams' launches (three batches in flight):
+// a rank-GEMM block of 4 waves at 152 VGPRs leaves each SIMD room for two waves of another stream's prep, which the
+// 8-wave form (round 4: 8 waves of 32 x 64 at 114 VGPRs, four waves per SIMD, 456 of 512 VGPRs) left none -- alone
+// it is slower (42 vs 36 us per batch of 8), beside the preps the headline gains 4-5% (1.18 vs 1.13e11 pairs/s,
+// round 5).  Split-bf16 (whose ring holds both planes) takes 128 x 64; kernel studies: CMVE_BATCH_GEO = 1288 (the
+// 8-wave 128 x 128), 256128 (256 x 128, one block per CU), 64 / 12864 (64 x 64 / 128 x 64).
 static int batch_geo_force() {
   static const int force = [] {
     const char* e = getenv("CMVE_BATCH_GEO");
@@ -2284,17 +2340,17 @@ static int batch_geo_bn(int64_t nq_pad, int64_t ng_pad, int mode) {
   return (f != 64 && f != 12864 && nq_pad % 128 == 0 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3) ? 128 : 64;
 }
 
-template <int MODE, int WN, int TM>
+template <int MODE, int WN, int TM, int WM = 4>
 static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
                              hipStream_t stream) {
-  using G = Geo<4, WN, TM>;
-  const size_t lds = ring_stages<MODE, G::BM, G::BN, false, G::NW>() * stage_bytes<MODE, G::BM, G::BN, false>();
+  using G = Geo<WM, WN, TM>;
+  const size_t lds = ring_lds_bytes<MODE, G::BM, G::BN, false, G::NW>();
   static const hipError_t attr_err = hipFuncSetAttribute(
-      (const void*)sim_kernel<MODE, EPI_RANK, 4, WN, TM, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (const void*)sim_kernel<MODE, EPI_RANK, WM, WN, TM, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)lds);
   CMVE_HIP(attr_err);
   const unsigned nblocks = (unsigned)((nq_pad / G::BM) * (ng_pad / G::BN));
-  cmve::launch(sim_kernel<MODE, EPI_RANK, 4, WN, TM, false, true>, dim3(nblocks, (unsigned)count), dim3(G::NT),
+  cmve::launch(sim_kernel<MODE, EPI_RANK, WM, WN, TM, false, true>, dim3(nblocks, (unsigned)count), dim3(G::NT),
                (uint32_t)lds, stream, SimArgs{}, tab);
   return check_launch("sim_kernel (batch)");
 }
@@ -2303,7 +2359,9 @@ static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int6
                              int bm, int bn, hipStream_t stream) {
   if constexpr (MODE != CMVE_SIM_BF16X3) {
     if (bm == 256 && bn == 128) return launch_rank_batch<MODE, 2, 4>(tab, count, nq_pad, ng_pad, stream);
-    if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
+    if (bm == 128 && bn == 128 && batch_geo_force() == 1288)  // (8 waves of 32 x 64: round 4's geometry)
+      return launch_rank_batch<MODE, 2, 2>(tab, count, nq_pad, ng_pad, stream);
+    if (bm == 128 && bn == 128) return launch_rank_batch<MODE, 2, 4, 2>(tab, count, nq_pad, ng_pad, stream);
   }
   return bm == 128 ? launch_rank_batch<MODE, 1, 2>(tab, count, nq_pad, ng_pad, stream)
                    : launch_rank_batch<MODE, 1, 1>(tab, count, nq_pad, ng_pad, stream);
