@@ -6,6 +6,7 @@ GPU every entry point raises.
 """
 from __future__ import annotations
 
+import atexit
 import contextlib
 import ctypes as C
 from typing import Dict, Optional, Sequence, Tuple
@@ -17,6 +18,19 @@ from . import _lib
 from ._lib import lib, check, Rows
 
 _HANDLES: Dict[Tuple[int, int], int] = {}
+
+# Set by an atexit hook: objects still alive when the interpreter exits (a batch table, a captured graph held by a
+# module or a test's traceback) skip their HIP destroy calls in __del__ -- the HIP runtime may already be torn down
+# then, and the process releases the device memory anyway.
+_EXITING = False
+
+
+def _mark_exiting():
+    global _EXITING
+    _EXITING = True
+
+
+atexit.register(_mark_exiting)
 
 
 def require_gpu():
@@ -284,6 +298,15 @@ class RankWorkspace:
         self.cand = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
         self.count = torch.zeros(_lib.MAX_CHUNKS, dtype=torch.int64, device=device)
         self.chunks = 1
+        self.scratch = None  # the tiled fix-up's sorted copy (cmve_rank_fixup_tiled), allocated on first use
+
+    def tiled_scratch(self, q: "RowSet", g: "RowSet", group: int) -> torch.Tensor:
+        need = int(lib.cmve_rank_fixup_tiled_scratch(C.byref(q.desc), C.byref(g.desc), self.cap, int(group)))
+        if need < 0:
+            raise _lib.CmveError("cmve_rank_fixup_tiled_scratch: bad arguments")
+        if self.scratch is None or self.scratch.numel() < need:
+            self.scratch = torch.empty(need, dtype=torch.int64, device=self.device)
+        return self.scratch
 
     @property
     def cap(self):
@@ -313,10 +336,12 @@ def rank_thresholds(a: RowSet, b: RowSet, sgt: torch.Tensor, mode: int):
 
 
 def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: Optional[RankWorkspace] = None,
-                      row_cnt=None, col_cnt=None, events=None, chunks: int = 1):
+                      row_cnt=None, col_cnt=None, events=None, chunks: int = 1, tiled: Optional[int] = None):
     """Enqueue the fused rank count (no sync).  row/col = (sgt, thr_hi, thr_lo) or None.
     chunks > 1: cmve_rank_count_overlap -- the gallery in `chunks` pieces, each piece's fp64
     fix-up on the handle's auxiliary stream behind the next piece's MFMA pass.
+    tiled = G >= 0 (chunks == 1): the fix-up regroups the pairs by (G gallery buckets, query tile) first
+    (cmve_rank_fixup_tiled; G = 0 picks the group size), for lists with many pairs per query tile.
     events = (start, mid, end) torch.cuda.Event triple recorded around the MFMA pass and the
     fix-up (with chunks > 1 the two overlap: mid is recorded with end)."""
     dirs = (_lib.DIR_ROW if row is not None else 0) | (_lib.DIR_COL if col is not None else 0)
@@ -345,8 +370,14 @@ def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: O
           "cmve_rank_mfma")
     if events is not None:
         events[1].record()
-    check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(row_cnt),
-                              _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)), "cmve_rank_fixup")
+    if tiled is not None and tiled >= 0:
+        sc = ws.tiled_scratch(q, g, tiled)
+        check(lib.cmve_rank_fixup_tiled(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]),
+                                        _ptr(row_cnt), _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count),
+                                        _ptr(sc), sc.numel(), int(tiled)), "cmve_rank_fixup_tiled")
+    else:
+        check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(row_cnt),
+                                  _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)), "cmve_rank_fixup")
     if events is not None:
         events[2].record()
     return row_cnt, col_cnt
@@ -668,9 +699,35 @@ class RankBatch:
         else:
             check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
 
+    def run_chained(self, prev: Optional["RankBatch"] = None, timing_slot: int = -1, wait_current: bool = True):
+        """Enqueue the batch with its finish (the words of its outputs: ranks, R@K) deferred to the next chained run on
+        the same stream, whose first launch holds it beside that run's prep (``cmve_eval_batch_run_chained``); ``prev``
+        is the batch chained before this one on the stream (its outputs are complete once this run's first launch
+        has run), None for the first.  After a stream's last chained run call ``finish()``.  ``prev`` must share no
+        session with this batch."""
+        if not self._b or (prev is not None and not prev._b):
+            raise RuntimeError("RankBatch.run_chained: a batch was closed")
+        if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
+            raise RuntimeError("RankBatch.run_chained: a session's workspace was regrown after the batch was built")
+        if self.stream is not None and wait_current:
+            cur = torch.cuda.current_stream(self.sessions[0].device)
+            if cur.cuda_stream != self.stream.cuda_stream:
+                self.stream.wait_stream(cur)
+        h = self._h if self._h is not None else handle(self.sessions[0].device)
+        check(lib.cmve_eval_batch_run_chained(h, self._b, prev._b if prev is not None else None, int(timing_slot)),
+              "cmve_eval_batch_run_chained")
+
+    def finish(self):
+        """The deferred finish of this batch's last chained run, alone (``cmve_eval_batch_finish``)."""
+        if not self._b:
+            raise RuntimeError("RankBatch.finish: the batch was closed")
+        h = self._h if self._h is not None else handle(self.sessions[0].device)
+        check(lib.cmve_eval_batch_finish(h, self._b), "cmve_eval_batch_finish")
+
     def kernel_timing(self, slot: int):
         """(prep, rank GEMM, 0, finish) durations in ms of the batch run that used `slot` (each launch's own
-        start / stop: the whole batch's launches)."""
+        start / stop: the whole batch's launches; a chained run: the prep launch holds the previous batch's finish,
+        and finish is 0)."""
         ms = (C.c_float * 4)()
         h = self._h if self._h is not None else handle(self.sessions[0].device)
         check(lib.cmve_eval_kernel_timing(h, int(slot), ms), "cmve_eval_kernel_timing")
@@ -678,9 +735,9 @@ class RankBatch:
 
     def close(self):
         if self._b:
-            lib.cmve_eval_batch_destroy(self._b)
+            if not _EXITING:  # (past interpreter exit the HIP runtime may be gone: the process releases the table)
+                lib.cmve_eval_batch_destroy(self._b)
             self._b = None
-
 
     def __del__(self):
         try:
@@ -713,7 +770,8 @@ class EvalGraph:
 
     def close(self):
         if self._g:
-            lib.cmve_eval_graph_destroy(self._g)
+            if not _EXITING:
+                lib.cmve_eval_graph_destroy(self._g)
             self._g = None
 
     def __del__(self):
@@ -882,10 +940,11 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
 
 def cu_mask_stream(device, cus):
     """A torch stream (ExternalStream over a HIP stream of libcmve.so's) whose kernels run only on the CUs in
-    ``cus`` (indices into the device's CUs, at least one: ``cmve_stream_create_cu_mask``).  The HIP stream is
-    destroyed (``cmve_stream_destroy``) when the returned object is garbage-collected or passed to
-    ``close_cu_mask_stream``, whichever comes first; synchronise it before dropping it."""
-    import weakref
+    ``cus`` (indices into the device's CUs, at least one: ``cmve_stream_create_cu_mask``).  Destroy it with
+    ``close_cu_mask_stream`` once every tensor recorded on it is freed (a RankSession on this stream records the
+    inputs it reads in place: the caching allocator records an event on the stream when such a tensor is freed,
+    so the stream must outlive them).  Never destroyed behind the caller's back: a stream still open at exit is
+    released with the process."""
     import torch
     dev = torch.device(device)
     n = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -901,20 +960,19 @@ def cu_mask_stream(device, cus):
     ptr = C.c_void_p()
     with torch.cuda.device(dev):
         check(lib.cmve_stream_create_cu_mask(mask, words, C.byref(ptr)), "cmve_stream_create_cu_mask")
-    st = torch.cuda.ExternalStream(ptr.value, device=dev)
-    fin = weakref.finalize(st, lib.cmve_stream_destroy, C.c_void_p(ptr.value))
-    fin.atexit = False  # (at interpreter exit the HIP runtime may already be torn down: the process releases it)
-    _CU_STREAMS[ptr.value] = fin
-    return st
+    _CU_STREAMS.add(ptr.value)
+    return torch.cuda.ExternalStream(ptr.value, device=dev)
 
 
-_CU_STREAMS = {}
+_CU_STREAMS = set()  # HIP streams made by cu_mask_stream and not yet closed
 
 
 def close_cu_mask_stream(stream):
-    """Destroy a ``cu_mask_stream`` now (after synchronising it); later uses of the object are errors."""
-    fin = _CU_STREAMS.pop(stream.cuda_stream, None)
-    if fin is None:
+    """Destroy a ``cu_mask_stream`` now (after synchronising it); later uses of the object are errors.  Free the
+    tensors recorded on the stream first (see cu_mask_stream)."""
+    p = stream.cuda_stream
+    if p not in _CU_STREAMS:
         raise ValueError("close_cu_mask_stream: not a live cu_mask_stream")
     stream.synchronize()
-    fin()
+    _CU_STREAMS.discard(p)
+    check(lib.cmve_stream_destroy(C.c_void_p(p)), "cmve_stream_destroy")

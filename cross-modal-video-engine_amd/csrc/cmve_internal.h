@@ -22,6 +22,7 @@ struct cmve_handle {
   // kernel-exact timing of the same evaluations: start / stop of each of the four launches
   hipEvent_t eval_kev[CMVE_EVAL_TIMING_SLOTS][8] = {};
   bool eval_no_fix[CMVE_EVAL_TIMING_SLOTS] = {};  // the slot's evaluation had no fix-up launch (re-scored in the GEMM)
+  bool eval_chained[CMVE_EVAL_TIMING_SLOTS] = {};  // the slot's batch ran chained (its finish in the next run's launch)
   // grow-only device scratch (split-K partials of cmve_gemm_f32); grown outside the hot loop
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -156,7 +157,9 @@ __host__ __device__ __forceinline__ bool rows_vec4(const T* p, int64_t d, int64_
 // trip so eight 16-B (fp32) or sixteen 16-B (fp64) loads are in flight (the fix-up re-scores random
 // pairs: latency, not arithmetic, bounds it).  The order is a function of the pair alone (not of
 // the element types) and symmetric in (a, b), so every caller gets the same bits for the same pair.
-template <typename TA, typename TB>
+// LIGHT: the same chain with half the loads in flight (two 256-element strides at a time): the same bits at half the
+// registers, for kernels whose register budget the rare fp64 re-score must not set (the chained prep + finish)
+template <typename TA, typename TB, bool LIGHT = false>
 __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB* __restrict__ b,
                                              int64_t d, int lane) {
   double acc = 0.0;
@@ -167,6 +170,20 @@ __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB*
     };
     int64_t k = (int64_t)lane * 4;
     for (; k + 768 < d; k += 1024) {
+      if constexpr (LIGHT) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          double a0[4], a1[4], b0[4], b1[4];
+          load4d(a + k + 512 * h, a0);
+          load4d(a + k + 512 * h + 256, a1);
+          load4d(b + k + 512 * h, b0);
+          load4d(b + k + 512 * h + 256, b1);
+          fma4(a0, b0);
+          fma4(a1, b1);
+          __builtin_amdgcn_sched_barrier(0);  // (the next half's loads stay below this half's fmas)
+        }
+        continue;
+      }
       double a0[4], a1[4], a2[4], a3[4], b0[4], b1[4], b2[4], b3[4];
       load4d(a + k, a0);
       load4d(a + k + 256, a1);
@@ -181,11 +198,19 @@ __device__ __forceinline__ double wave_dot64(const TA* __restrict__ a, const TB*
       fma4(a2, b2);
       fma4(a3, b3);
     }
-    for (; k < d; k += 256) {
-      double x[4], y[4];
-      load4d(a + k, x);
-      load4d(b + k, y);
-      fma4(x, y);
+    {
+      // the last (at most three) 256-element strides with every load in flight before the fmas, which keep the
+      // stride order (the same bits): a 640-element row (C4) is one round trip instead of three
+      double x[3][4], y[3][4];
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+        if (k + 256 * m < d) {
+          load4d(a + k + 256 * m, x[m]);
+          load4d(b + k + 256 * m, y[m]);
+        }
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+        if (k + 256 * m < d) fma4(x[m], y[m]);
     }
     return wave_sum(acc);
   }
@@ -432,10 +457,10 @@ constexpr int EVAL_EMAX_SHARDS = 64;  // K14: err_max shards per side and plane 
 
 // canonical exact score: cos64(x, y) = dot64(raw_x, raw_y) * (inv_x * inv_y), symmetric in (x, y), so
 // the GT-score, fix-up and top-k re-score kernels score a pair bit-identically
-template <typename TA, typename TB>
+template <typename TA, typename TB, bool LIGHT = false>
 __device__ __forceinline__ double wave_cos64(const TA* xa, const TB* xb, double inva, double invb, int64_t d,
                                              int lane) {
-  return wave_dot64(xa, xb, d, lane) * (inva * invb);
+  return wave_dot64<TA, TB, LIGHT>(xa, xb, d, lane) * (inva * invb);
 }
 
 // ---- K14 level-2 re-score: one pair's score from the fp16 + bf16 residual planes (lo16_elem, cmve_internal.h) ----
@@ -543,7 +568,9 @@ __device__ __forceinline__ void fixup_prefix(const uint64_t* __restrict__ cand, 
   }
 }
 
-template <typename TQ, typename TG, bool PREFETCH = false>
+// DYN_PRE: the bucket prefix in dynamic LDS sized by the launch ((buckets per group + 1) * 8 bytes) instead of the
+// 32 KiB static array, which capped the fix-up at 5 blocks per CU whatever its registers allowed
+template <typename TQ, typename TG, bool PREFETCH = false, bool DYN_PRE = false, bool LIGHT = false>
 __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
                                                     int64_t ldg, const double* __restrict__ ginv, int64_t d,
@@ -552,7 +579,14 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
                                                     int64_t nb, int64_t cap_b, bool flat = false,
                                                     const L2Planes l2 = L2Planes{}) {
-  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+  int64_t* pre;
+  if constexpr (DYN_PRE) {
+    extern __shared__ int64_t fix_dyn_pre[];
+    pre = fix_dyn_pre;
+  } else {
+    __shared__ int64_t fix_pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+    pre = fix_pre;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = flat ? 1 : 8;  // bucket groups (XCDs)
   const int xcd = flat ? 0 : (blockIdx.x & 7);
@@ -614,7 +648,7 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
       rs = ((flags & 1u) && row_sgt) ? gld(row_sgt + i) : 0.0;
       cs = ((flags & 2u) && col_sgt) ? gld(col_sgt + j) : 0.0;
     }
-    const double s = wave_cos64(qraw + i * ldq, graw + j * ldg, gld(qinv + i), gld(ginv + j), d, lane);
+    const double s = wave_cos64<TQ, TG, LIGHT>(qraw + i * ldq, graw + j * ldg, gld(qinv + i), gld(ginv + j), d, lane);
     if (lane == 0) {
       if ((flags & 1u) && row_sgt && s > (PREFETCH ? rs : gld(row_sgt + i))) gadd(row_cnt + i, 1);
       if ((flags & 2u) && col_sgt && s > (PREFETCH ? cs : gld(col_sgt + j))) gadd(col_cnt + j, 1);

@@ -546,14 +546,17 @@ __device__ __forceinline__ void load_row_buf(const float* row, int lane, double 
 }
 
 template <typename TQ, typename TG, int NM>
-__device__ __forceinline__ void eval_prep_pair_f16_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+__device__ __forceinline__ void eval_prep_pair_f16_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c,
+                                                        int64_t vb, int64_t nvb) {
+  // vb / nvb: this block and the prep's block count (blockIdx.x / gridDim.x, or the prep blocks' own numbering in
+  // eval_prep_fin_batch_kernel)
   EVAL_STAMP(c, 0, 0);
   const int lane = threadIdx.x & 63;
-  const int64_t i = (int64_t)blockIdx.x * PREP_NW + (threadIdx.x >> 6);
-  for (int64_t t = (int64_t)blockIdx.x * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)gridDim.x * PREP_NT)
+  const int64_t i = (int64_t)vb * PREP_NW + (threadIdx.x >> 6);
+  for (int64_t t = (int64_t)vb * PREP_NT + threadIdx.x; t < c.nb; t += (int64_t)nvb * PREP_NT)
     gst(c.bucket + t, 0ull);
-  if (blockIdx.x == 0 && threadIdx.x < 13) gst(c.stats + threadIdx.x, 0);  // the finish blocks add into it
-  if (blockIdx.x == 0 && threadIdx.x == 0 && c.l3_count) gst(c.l3_count, 0u);  // the rank GEMM appends level 3
+  if (vb == 0 && threadIdx.x < 13) gst(c.stats + threadIdx.x, 0);  // the finish blocks add into it
+  if (vb == 0 && threadIdx.x == 0 && c.l3_count) gst(c.l3_count, 0u);  // the rank GEMM appends level 3
   float ebq[3] = {0.f, 0.f, 0.f}, ebg[3] = {0.f, 0.f, 0.f};
   if (i < q.n_pad && !(c.dbg & 1)) {
     if (i >= q.n) {  // padding rows of both sides: zero vectors, zero bounds, never counted
@@ -629,7 +632,7 @@ __device__ __forceinline__ void eval_prep_pair_f16_body(const EvalSide& q, const
     float m = 0.f;
 #pragma unroll
     for (int w = 0; w < PREP_NW; ++w) m = fmaxf(m, s_eb[w][threadIdx.x]);
-    unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + blockIdx.x % EMAX_SHARDS];  // [side][plane] = tid
+    unsigned* sh = &c.emax[threadIdx.x * EMAX_SHARDS + vb % EMAX_SHARDS];  // [side][plane] = tid
     if (c.dbg & 2) {  // kernel studies only: no err_max shards (results garbage)
     } else if (m == INFINITY) gst(sh, __float_as_uint(m));
     else if (m > 0.f) gmax(sh, __float_as_uint(m));
@@ -789,21 +792,23 @@ __device__ __forceinline__ void finish_err_max(const EvalSide& q, const EvalSide
 
 // The ranks of both directions (cmve_gt_ranks' rules) for this block's 256 rows of each side and, per
 // direction, #rank<=1, <=5, <=10 and the rank sum, added into the stats head (zeroed by the prep)
-template <typename TQ, typename TG>
-__device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
+template <typename TQ, typename TG, bool LIGHT = false>
+__device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int64_t vb,
+                                                 int64_t nvb) {
+  // vb / nvb: this block and the finish's block count (eval_prep_pair_f16_body's convention)
   EVAL_STAMP(c, 1, 0);
   if (c.dbg & 32) return;
   __shared__ unsigned long long red[9 * FIN_NW];
-  const unsigned nrank = gridDim.x - 2;  // the last two blocks: pair total / overflow, err_max
-  if (blockIdx.x >= nrank) {
-    if (blockIdx.x == nrank) finish_buckets(c);
+  const int64_t nrank = nvb - 2;  // the last two blocks: pair total / overflow, err_max
+  if (vb >= nrank) {
+    if (vb == nrank) finish_buckets(c);
     else finish_err_max(q, g, c);
     EVAL_STAMP(c, 1, 1);
     return;
   }
   // per wave: #rank <= 1 / 5 / 10 from ballots (no reduction), the rank sums in one butterfly of both
   // directions; then one LDS round over the block's waves and 8 lanes adding into the stats head
-  const int64_t i = (int64_t)blockIdx.x * FIN_NT + threadIdx.x;
+  const int64_t i = (int64_t)vb * FIN_NT + threadIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // level 3, deferred by the rank GEMM (EvalCommon::l3): the listed pairs whose row (t2v) or column (v2t) is one
   // of this block's, re-scored in fp64 by wave_cos64 (the fix-up's arithmetic: the same bits as an inline
@@ -831,7 +836,7 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
     add_q[threadIdx.x] = 0;
     add_g[threadIdx.x] = 0;
     __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * FIN_NT;
+    const int64_t r0 = (int64_t)vb * FIN_NT;
     for (unsigned e = (unsigned)wave; e < n3; e += FIN_NW) {
       const uint64_t u = e == (unsigned)wave ? u_first : gld(c.l3 + e);
       const int64_t pi = (int64_t)(u & 0x7fffffffull), pj = (int64_t)((u >> 31) & 0x7fffffffull);
@@ -839,7 +844,7 @@ __device__ __forceinline__ void eval_finish_body(const EvalSide& q, const EvalSi
       const bool mq = (fl & 1u) && pi >= r0 && pi < r0 + FIN_NT;
       const bool mg = (fl & 2u) && pj >= r0 && pj < r0 + FIN_NT;
       if (!(mq || mg)) continue;  // (wave-uniform)
-      const double sc = wave_cos64((const TQ*)q.raw + pi * q.ld, (const TG*)g.raw + pj * g.ld, gld(q.inv + pi),
+      const double sc = wave_cos64<TQ, TG, LIGHT>((const TQ*)q.raw + pi * q.ld, (const TG*)g.raw + pj * g.ld, gld(q.inv + pi),
                                    gld(g.inv + pj), c.d, lane);
       if (lane == 0) {
         if (mq && sc > gld(q.sgt + pi)) atomicAdd(&add_q[pi - r0], 1);
@@ -903,7 +908,7 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_kernel(EvalSide q, Eva
 }
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(FIN_NT) void eval_finish_kernel(EvalSide q, EvalSide g, EvalCommon c) {
-  eval_finish_body<TQ, TG>(q, g, c);
+  eval_finish_body<TQ, TG>(q, g, c, blockIdx.x, gridDim.x);
 }
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(PREP_NT) void eval_prep_batch_kernel(const EvalItem* __restrict__ tab) {
@@ -920,17 +925,39 @@ __global__ __launch_bounds__(PREP_NT) void eval_prep_pair_batch_kernel(const Eva
 #endif
 template <typename TQ, typename TG, int NM>
 __global__ __launch_bounds__(PREP_NT, CMVE_PREP_WPE) void eval_prep_pair_f16_kernel(EvalSide q, EvalSide g, EvalCommon c) {
-  eval_prep_pair_f16_body<TQ, TG, NM>(q, g, c);
+  eval_prep_pair_f16_body<TQ, TG, NM>(q, g, c, blockIdx.x, gridDim.x);
 }
 template <typename TQ, typename TG, int NM>
 __global__ __launch_bounds__(PREP_NT, CMVE_PREP_WPE) void eval_prep_pair_f16_batch_kernel(const EvalItem* __restrict__ tab) {
   const EvalItem& it = tab[blockIdx.y];
-  eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c);
+  eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c, blockIdx.x, gridDim.x);
 }
 template <typename TQ, typename TG>
 __global__ __launch_bounds__(FIN_NT) void eval_finish_batch_kernel(const EvalItem* __restrict__ tab) {
   const EvalItem& it = tab[blockIdx.y];
-  eval_finish_body<TQ, TG>(it.q, it.g, it.c);
+  eval_finish_body<TQ, TG>(it.q, it.g, it.c, blockIdx.x, gridDim.x);
+}
+// The chained batch launch (cmve_eval_batch_run_chained): the specialised prep of a batch and the finish of the
+// batch run before it on the same stream in ONE launch -- row y of the grid: blocks [0, nprep) the prep of
+// evaluation y of ptab, blocks [nprep, nprep + nfin) the finish of evaluation y of ftab (no ftab: those blocks
+// return).  The two roles touch different workspaces (the caller checks), and the finish's inputs were complete
+// when the previous batch's rank GEMM ended, before this launch: one launch per batch fewer on the stream, and
+// the finish's few blocks run in the prep's shadow instead of as a launch of their own between two batches.
+template <typename TQ, typename TG, int NM>
+#ifndef CMVE_PREPFIN_WPE
+#define CMVE_PREPFIN_WPE 4  // (the finish role takes the light fp64 re-score: the full one alone took 114 registers,
+#endif                      // and a launch above 104 fits one wave per SIMD beside the batch rank GEMM's two, not two)
+__global__ __launch_bounds__(PREP_NT, CMVE_PREPFIN_WPE) void eval_prep_fin_batch_kernel(const EvalItem* __restrict__ ptab,
+                                                                                    const EvalItem* __restrict__ ftab,
+                                                                                    int nprep, int nfin) {
+  static_assert(PREP_NT == FIN_NT, "one block size for both roles");
+  if ((int)blockIdx.x < nprep) {
+    const EvalItem& it = ptab[blockIdx.y];
+    eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c, blockIdx.x, nprep);
+  } else if (ftab) {
+    const EvalItem& it = ftab[blockIdx.y];
+    eval_finish_body<TQ, TG, true>(it.q, it.g, it.c, (int)blockIdx.x - nprep, nfin);
+  }
 }
 
 // the specialized paired prep applies: F16 with the lo16 plane, 16-B row pieces, d = d_pad = 256 NM (NM <= 4)
@@ -975,6 +1002,32 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
                dim3(FIN_NT), 0u, s, tab);
   return check_launch("eval_finish_batch_kernel");
 }
+
+template <typename TQ, typename TG>
+static int launch_eval_batch_chained_typed(const EvalSide& q, const EvalSide& g, const EvalCommon& c0,
+                                           const EvalItem* ptab, const EvalItem* ftab, int count, hipStream_t s) {
+  const int nm = prep_f16_nm(q, g, c0);
+  CMVE_REQUIRE(nm, "launch_eval_batch_chained: the batch does not take the specialised paired prep");
+  const int nprep = (int)((q.n_pad + PREP_NW - 1) / PREP_NW);
+  const int64_t nmax = q.n > g.n ? q.n : g.n;
+  const int nfin = (int)((nmax + FIN_NT - 1) / FIN_NT) + 2;
+  CMVE_PREP_F16(eval_prep_fin_batch_kernel, nm, dim3((unsigned)(nprep + (ftab ? nfin : 0)), (unsigned)count),
+                dim3(PREP_NT), 0u, s, ptab, ftab, nprep, nfin);
+  return check_launch("eval_prep_fin_batch_kernel");
+}
+
+// the specialised paired prep of `ptab` and the finish of `ftab` (nullptr: none) in one launch; both batches have
+// the shapes of q / g / c0 and `count` evaluations
+int launch_eval_batch_chained(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* ptab,
+                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s) {
+  if (!q_f64 && !g_f64) return launch_eval_batch_chained_typed<float, float>(q, g, c0, ptab, ftab, count, s);
+  if (!q_f64 && g_f64) return launch_eval_batch_chained_typed<float, double>(q, g, c0, ptab, ftab, count, s);
+  if (q_f64 && !g_f64) return launch_eval_batch_chained_typed<double, float>(q, g, c0, ptab, ftab, count, s);
+  return launch_eval_batch_chained_typed<double, double>(q, g, c0, ptab, ftab, count, s);
+}
+
+// whether a batch of these shapes takes launch_eval_batch_chained
+bool eval_batch_chainable(const EvalSide& q, const EvalSide& g, const EvalCommon& c0) { return prep_f16_nm(q, g, c0) != 0; }
 
 // a batch: the items share q / g shapes, dtypes and GT lists (tab[i] differ in buffers only); phases 0 / 2 / 3
 // as launch_eval (no separate fix-up: the batch path is the G64 inline fix-up geometry)

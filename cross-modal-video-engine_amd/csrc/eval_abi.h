@@ -60,7 +60,7 @@ struct EvalCommon {
 // phase 0: pack + GT scores, phase 1: fix-up, phase 2: err_max + ranks + R@K (the rank GEMM runs between
 // phases 0 and 1, sim.hip); stamp k of block b in kernel kern (0 prep, 1 finish, 2 fix-up) when stamps are on
 #define EVAL_STAMP(cp, kern, k)                                                                                  \
-  if ((cp).stamps && threadIdx.x == 0)                                                                           \
+  if ((cp).stamps && threadIdx.x == 0 && blockIdx.x < 1024)                                                     \
   (cp).stamps[((size_t)(kern) * 1024 + blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
 int launch_eval(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int q_f64, int g_f64, int phase,
                 hipStream_t s);
@@ -69,6 +69,9 @@ struct EvalItem {
   EvalSide q, g;
   EvalCommon c;
 };
+int launch_eval_batch_chained(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* ptab,
+                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s);
+bool eval_batch_chainable(const EvalSide& q, const EvalSide& g, const EvalCommon& c0);
 int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* tab, int count,
                       int q_f64, int g_f64, int phase, hipStream_t s);
 

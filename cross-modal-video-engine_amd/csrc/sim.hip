@@ -19,6 +19,7 @@
 // swizzle applied to the GLOBAL source chunk (chunk ^ (row & 7)) and the matching
 // ds_read_b128 address.  Grid: XCD-aware -- each XCD gets a contiguous range of the logical
 // tile order, which walks 8 gallery tiles x all query tiles.
+#include <algorithm>
 #include <vector>
 
 #include <hip/hip_ext.h>
@@ -1692,6 +1693,10 @@ int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* can
 int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs, const double* row_sgt,
                  const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t cand_cap,
                  const int64_t* cand_count);
+int64_t fixup_tiled_scratch_words(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int group);
+int launch_fixup_tiled(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
+                       const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
+                       const uint64_t* cand, int64_t cand_cap, uint64_t* scratch, int64_t scratch_cap, int group);
 }
 
 // point the epilogue at the bucketed layout of `cand` (cand_layout) for the gallery view g
@@ -1788,6 +1793,28 @@ extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve
   if (q->n == 0 || g->n == 0) return CMVE_OK;  // nothing to re-score (an empty gallery shard)
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup: raw rows / norms missing");
   return launch_fixup(h->stream, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, cand_count);
+}
+
+extern "C" int64_t cmve_rank_fixup_tiled_scratch(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap,
+                                                 int32_t group) {
+  if (!q || !g || cand_cap < 0) return -1;
+  return fixup_tiled_scratch_words(q, g, cand_cap, group);
+}
+
+extern "C" int cmve_rank_fixup_tiled(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
+                                     const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
+                                     const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count,
+                                     uint64_t* scratch, int64_t scratch_cap, int32_t group) {
+  CMVE_REQUIRE(h && q && g, "cmve_rank_fixup_tiled: NULL argument");
+  CMVE_REQUIRE(q->d == g->d, "cmve_rank_fixup_tiled: dimension mismatch");
+  if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_sgt && row_cnt, "cmve_rank_fixup_tiled: row arrays missing");
+  if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_sgt && col_cnt, "cmve_rank_fixup_tiled: col arrays missing");
+  CMVE_REQUIRE(cand && cand_count && scratch, "cmve_rank_fixup_tiled: candidate / scratch buffer missing");
+  CMVE_REQUIRE(group >= 0 && group <= 64, "cmve_rank_fixup_tiled: group must be 0 (auto) .. 64");
+  if (q->n == 0 || g->n == 0) return CMVE_OK;
+  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup_tiled: raw rows / norms missing");
+  return launch_fixup_tiled(h->stream, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, scratch,
+                            scratch_cap, group);
 }
 
 extern "C" int cmve_rank_count(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs,
@@ -2283,7 +2310,10 @@ extern "C" int cmve_eval_ranks(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, 
   st = dispatch<EPI_RANK>(a, q, g, mode, s);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  if (timing_slot >= 0) h->eval_no_fix[timing_slot] = P.inline_fix && !P.fix_launch;
+  if (timing_slot >= 0) {
+    h->eval_no_fix[timing_slot] = P.inline_fix && !P.fix_launch;
+    h->eval_chained[timing_slot] = false;
+  }
   if (!P.inline_fix || P.fix_launch) {
     arm(2);
     st = cmve::launch_eval(P.sq, P.sg, P.c, P.qf, P.gf, 1, s);
@@ -2311,6 +2341,8 @@ struct cmve_eval_batch {
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
   hipEvent_t ev_in = nullptr, ev_prep = nullptr;  // cmve_eval_batch_run_split's stream hand-offs
+  std::vector<void*> ws;          // the evaluations' workspaces (a chained run refuses a previous batch sharing one)
+  bool chainable = false;         // the specialised paired prep: the chained run fuses it with the previous finish
 };
 
 // the batch's rank geometry: 128 x 128 tiles on 4 waves of 64 x 64 (a 2-stage ring of 32 KiB stages, two blocks of
@@ -2432,6 +2464,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->sg0 = P0.sg;
   b->c0 = P0.c;
   b->fix_launch = P0.fix_launch;
+  b->ws.assign(ws, ws + count);
+  b->chainable = cmve::eval_batch_chainable(P0.sq, P0.sg, P0.c);
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
   if (e == hipSuccess) e = hipMalloc(&b->d_args, sizeof(SimArgs) * (size_t)count);
   if (e == hipSuccess)
@@ -2451,7 +2485,8 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
 // prep, rank GEMM, 0, finish -- durations of the whole batch's launches) and the event spans (cmve_eval_timing)
 // ps: the prep launch's stream (h->stream, or cmve_eval_batch_run_split's prep stream: it first waits for the work
 // enqueued on h->stream, and the rank GEMM waits for the prep)
-static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, int32_t timing_slot) {
+static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, int32_t timing_slot,
+                          bool chained = false, cmve_eval_batch_t prev = nullptr) {
   hipEvent_t* ev = nullptr;
   hipEvent_t* kev = nullptr;
   if (timing_slot >= 0) {
@@ -2462,6 +2497,7 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, 
     for (int k = 0; k < 8; ++k)
       if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
     h->eval_no_fix[timing_slot] = !b->fix_launch;
+    h->eval_chained[timing_slot] = chained;
   }
   auto arm = [&](int k) {
     if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
@@ -2474,9 +2510,19 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, 
     CMVE_HIP(hipEventRecord(b->ev_in, s));  // (the batch's previous run and whatever the caller enqueued before)
     CMVE_HIP(hipStreamWaitEvent(ps, b->ev_in, 0));
   }
+  int st = CMVE_OK;
+  const bool fused = chained && b->chainable;  // the prep and the previous batch's finish in one launch
+  if (chained && prev && !fused) {  // (not the specialised prep: the previous batch's finish as a launch of its own)
+    st = cmve::launch_eval_batch(prev->sq0, prev->sg0, prev->c0, prev->d_items, prev->count, prev->qf, prev->gf, 2, ps);
+    if (st) return st;
+  }
   if (ev) CMVE_HIP(hipEventRecord(ev[0], ps));
   arm(0);
-  int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, ps);
+  if (fused)
+    st = cmve::launch_eval_batch_chained(b->sq0, b->sg0, b->c0, b->d_items, prev ? prev->d_items : nullptr, b->count,
+                                         b->qf, b->gf, ps);
+  else
+    st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, ps);
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[1], ps));
   if (split) {
@@ -2496,9 +2542,11 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, 
     st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 1, s);
     if (st) return st;
   }
-  arm(3);
-  st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, s);
-  if (st) return st;
+  if (!chained) {
+    arm(3);
+    st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, s);
+    if (st) return st;
+  }
   if (ev) CMVE_HIP(hipEventRecord(ev[3], s));
   return CMVE_OK;
 }
@@ -2507,6 +2555,30 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
   CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
   return eval_batch_run(h, b, h->stream, timing_slot);
+}
+
+extern "C" int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t b, cmve_eval_batch_t prev,
+                                           int32_t timing_slot) {
+  CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run_chained: NULL handle / batch");
+  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS,
+               "cmve_eval_batch_run_chained: bad timing slot");
+  if (prev) {
+    CMVE_REQUIRE(prev->d_items && prev != b, "cmve_eval_batch_run_chained: the previous batch is destroyed or the batch itself");
+    CMVE_REQUIRE(prev->count == b->count && prev->nq_pad == b->nq_pad && prev->ng_pad == b->ng_pad &&
+                     prev->sq0.n == b->sq0.n && prev->sg0.n == b->sg0.n && prev->qf == b->qf && prev->gf == b->gf &&
+                     prev->mode == b->mode && prev->paired == b->paired && prev->chainable == b->chainable,
+                 "cmve_eval_batch_run_chained: the previous batch differs in shape from the batch");
+    for (void* w : b->ws)
+      CMVE_REQUIRE(std::find(prev->ws.begin(), prev->ws.end(), w) == prev->ws.end(),
+                   "cmve_eval_batch_run_chained: the batch shares a workspace with the previous batch, whose finish "
+                   "runs in the same launch as its prep");
+  }
+  return eval_batch_run(h, b, h->stream, timing_slot, true, prev);
+}
+
+extern "C" int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t b) {
+  CMVE_REQUIRE(h && b && b->d_items, "cmve_eval_batch_finish: NULL handle / batch");
+  return cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, h->stream);
 }
 
 extern "C" int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t b, void* prep_stream, int32_t timing_slot) {
@@ -2603,11 +2675,13 @@ extern "C" int cmve_eval_timing(cmve_handle_t h, int32_t slot, float* ms3) {
 extern "C" int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4) {
   CMVE_REQUIRE(h && ms4 && slot >= 0 && slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_kernel_timing: bad argument");
   hipEvent_t* kev = h->eval_kev[slot];
-  CMVE_REQUIRE(kev[0] && kev[7], "cmve_eval_kernel_timing: slot %d never recorded", slot);
-  CMVE_HIP(hipEventSynchronize(kev[7]));
+  const bool chained = h->eval_chained[slot];  // (cmve_eval_batch_run_chained: the finish ran in the next run's prep)
+  const int last = chained ? (h->eval_no_fix[slot] ? 3 : 5) : 7;
+  CMVE_REQUIRE(kev[0] && kev[last], "cmve_eval_kernel_timing: slot %d never recorded", slot);
+  CMVE_HIP(hipEventSynchronize(kev[last]));
   for (int k = 0; k < 4; ++k) {
-    if (k == 2 && h->eval_no_fix[slot]) {  // no fix-up launch: its pairs were re-scored inside the rank GEMM
-      ms4[k] = 0.f;
+    if ((k == 2 && h->eval_no_fix[slot]) || (k == 3 && chained)) {  // no fix-up launch (re-scored in the rank GEMM) /
+      ms4[k] = 0.f;                                                  // the finish deferred to the next chained run
       continue;
     }
     CMVE_HIP(hipEventElapsedTime(&ms4[k], kev[2 * k], kev[2 * k + 1]));

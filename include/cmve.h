@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 19
+#define CMVE_ABI_VERSION 20
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -325,6 +325,19 @@ int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, 
 int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
                     const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
                     const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count);
+/* The same re-score with the undecided pairs first regrouped: `group` consecutive gallery buckets
+ * (0 = as many as keep their raw rows within 2 MiB) form a super-bucket whose pairs are counting-sorted
+ * by query tile into `scratch` (caller-owned, uint64[scratch_cap], scratch_cap >=
+ * cmve_rank_fixup_tiled_scratch(q, g, cand_cap, group)), so each query row is fetched once per
+ * (super-bucket, query tile) instead of once per pair.  For lists with many pairs per (query tile,
+ * gallery bucket) -- the MultiFusion CIRR ranking.  Counts identical to cmve_rank_fixup.
+ * Replaces: the argsort of MultiFusion/src/validate.py:71-105 (with cmve_rank_mfma). */
+int cmve_rank_fixup_tiled(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
+                          const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
+                          const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count,
+                          uint64_t* scratch, int64_t scratch_cap, int32_t group);
+/* scratch words cmve_rank_fixup_tiled needs (-1 on a NULL argument); no device work */
+int64_t cmve_rank_fixup_tiled_scratch(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int32_t group);
 
 /*
  * cmve_rank_count with the fix-up hidden behind the MFMA pass: the gallery `g` is cut into
@@ -451,6 +464,16 @@ int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch, int32_t timing
  * streams on disjoint CU sets (cmve_stream_create_cu_mask) one batch's HBM-bound prep runs beside another's rank
  * GEMM instead of taking every CU in turn.  Results are those of cmve_eval_batch_run. */
 int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t batch, void* prep_stream, int32_t timing_slot);
+/* Chained runs of a stream's successive batches (the headline's validation loop: LINAS-engine/validate.py:61-74 once
+ * per evaluation): the run of `batch` defers its finish (ranks, R@K, pair total: the outputs' words) to the next
+ * chained run on h's stream, whose first launch holds that finish beside its own prep (the specialised paired prep:
+ * one launch; otherwise the finish runs as a launch of its own first).  prev: the batch chained on this stream
+ * before (NULL: none); its outputs are complete once this call's first launch has run.  cmve_eval_batch_finish runs
+ * a batch's deferred finish alone (after a stream's last chained run).  prev must have the batch's shapes and share
+ * no workspace with it.  Results equal cmve_eval_batch_run's bit for bit; timing_slot records the launches
+ * (cmve_eval_kernel_timing: prep (with the previous finish), rank GEMM, fix-up, 0). */
+int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t batch, cmve_eval_batch_t prev, int32_t timing_slot);
+int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t batch);
 /* a HIP stream restricted to the CUs set in mask (bit i of word i / 32 = CU i; hipExtStreamCreateWithCUMask) */
 int cmve_stream_create_cu_mask(const uint32_t* mask, int32_t nwords, void** stream);
 int cmve_stream_destroy(void* stream);

@@ -11,7 +11,7 @@ HEADER = os.path.join(ROOT, "include", "cmve.h")
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(cmve_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(cmve_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_hot_path():
@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 19
+    assert _lib.lib.cmve_abi_version() == 20
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)

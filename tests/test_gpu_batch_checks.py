@@ -81,3 +81,100 @@ def test_paired_flag_with_lists_that_are_no_pairing(torch_cuda):
     torch.cuda.synchronize()
     assert [int(t.out[11]) for t in sess] == [3, 3]
     b.close()
+
+
+def _groups(torch, n_groups, per, seed=11):
+    """n_groups batches of `per` C1-shaped evaluations (set 0 of group 0 is the golden C1 set, the others perturbed
+    captions: the ranks differ per set)."""
+    from cmve import engine
+    v, c, rows, cols = _c1_lists()
+    rng = np.random.default_rng(seed)
+    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
+    groups = []
+    for gi in range(n_groups):
+        sets, sess = [], []
+        for j in range(per):
+            cj = c if (gi == 0 and j == 0) else c + rng.uniform(0.05, 0.6) * rng.standard_normal(c.shape)
+            sets.append((torch.from_numpy(cj).cuda(), torch.from_numpy(v).cuda()))
+            sess.append(engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64))
+        groups.append((sess, sets))
+    return groups, n_q
+
+
+@pytest.mark.parametrize("per", [8, 3])
+def test_rank_batch_chained_equals_run(golden, torch_cuda, per):
+    """Chained batch runs (cmve_eval_batch_run_chained: a batch's finish in the next run's prep launch) give every
+    output word of the batch's own run(); a batch's outputs are complete once the next chained run is enqueued;
+    the C1 set's ranks equal the reference's."""
+    torch = torch_cuda
+    from cmve import engine
+    groups, n_q = _groups(torch, 3, per)
+    batches, ref = [], []
+    for sess, sets in groups:
+        b = engine.RankBatch(sess, sets)
+        b.run()
+        torch.cuda.synchronize()
+        ref.append([s.out.clone() for s in sess])
+        for s in sess:  # (the chained runs must write every word an evaluation writes again; out[13:16] reserved)
+            s.out[:13].fill_(-7)
+            s.out[16:].fill_(-7)
+        batches.append(b)
+    g = golden("retrieval_c1")
+    h = ref[0][0].cpu().numpy()
+    assert np.array_equal(h[16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[16 + n_q:], g["v2t_ranks"])
+    prev = None
+    for k, bi in enumerate([0, 1, 2, 0, 1, 2, 1]):
+        batches[bi].run_chained(prev, timing_slot=k % 4)
+        if k == 1:
+            torch.cuda.synchronize()  # batch 0's finish ran in batch 1's first launch
+            for s, r in zip(groups[0][0], ref[0]):
+                assert torch.equal(s.out, r)
+        prev = batches[bi]
+    prev.finish()
+    torch.cuda.synchronize()
+    for (sess, _), rs in zip(groups, ref):
+        for s, r in zip(sess, rs):
+            assert torch.equal(s.out, r), (s.out[:16].tolist(), r[:16].tolist())
+    ms = batches[2].kernel_timing(3)
+    assert ms[0] > 0 and ms[1] > 0 and ms[3] == 0.0
+    twin = engine.RankBatch(groups[0][0][:per], groups[0][1][:per])
+    with pytest.raises(RuntimeError, match="shares a workspace"):
+        batches[0].run_chained(twin)
+    for b in batches + [twin]:
+        b.close()
+
+
+def test_rank_batch_chained_general_prep(torch_cuda):
+    """A batch that takes no specialised prep (multi-GT fp32 lists, split-bf16) chains through separate launches:
+    the previous finish first, then the prep and the rank GEMM -- outputs equal run()'s."""
+    torch = torch_cuda
+    from cmve import engine, _lib
+    rng = np.random.default_rng(21)
+    nq, ng, d = 700, 900, 384
+    rows = [[int(x) for x in rng.choice(ng, size=1 + i % 3, replace=False)] for i in range(nq)]
+    cols = [[] for _ in range(ng)]
+    for i, l in enumerate(rows):
+        for j in l:
+            cols[j].append(i)
+    bats, ref = [], []
+    for b in range(2):
+        sets, sess = [], []
+        for j in range(2):
+            gal = rng.standard_normal((ng, d)).astype(np.float32)
+            qs = (gal[[l[0] for l in rows]] + 0.9 * rng.standard_normal((nq, d))).astype(np.float32)
+            sets.append((torch.from_numpy(qs).cuda(), torch.from_numpy(gal).cuda()))
+            sess.append(engine.RankSession(nq, ng, d, row_gts=rows, col_gts=cols, dtype=torch.float32,
+                                           mode=_lib.SIM_BF16X3))
+        rb = engine.RankBatch(sess, sets)
+        rb.run()
+        torch.cuda.synchronize()
+        ref.append([s.out.clone() for s in sess])
+        bats.append((rb, sess))
+    bats[0][0].run_chained(None)
+    bats[1][0].run_chained(bats[0][0])
+    bats[1][0].finish()
+    torch.cuda.synchronize()
+    for (rb, sess), rs in zip(bats, ref):
+        for s, r in zip(sess, rs):
+            assert torch.equal(s.out, r)
+        rb.close()

@@ -903,6 +903,27 @@ def test_rank_batch_run_split_streams(golden, torch_cuda):
     h = sess[0].out.cpu().numpy()
     assert np.array_equal(h[16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[16 + n_q:], g["v2t_ranks"])
     b.close()
+    # (the streams stay open: the inputs read in place were recorded on gs, and the caching allocator records an
+    # event on it when they are freed -- test_cu_mask_stream_close closes a stream nothing was recorded on)
+
+
+@pytest.mark.gpu
+def test_cu_mask_stream_close(torch_cuda):
+    """cu_mask_stream refuses an empty CU list; close_cu_mask_stream destroys the stream once (a second close is an
+    error); work launched on it before the close completes."""
+    torch = torch_cuda
+    from cmve import engine
+    with pytest.raises(ValueError, match="no CU"):
+        engine.cu_mask_stream("cuda:0", [])
+    st = engine.cu_mask_stream("cuda:0", [0, 1, 2, 3])
+    x = torch.arange(1 << 20, device="cuda:0", dtype=torch.float32)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        y = x * 2.0
+    engine.close_cu_mask_stream(st)
+    assert float(y[-1]) == 2.0 * ((1 << 20) - 1)
+    with pytest.raises(ValueError, match="not a live"):
+        engine.close_cu_mask_stream(st)
 
 
 @pytest.mark.gpu

@@ -31,6 +31,7 @@ def role(name):
     profile holding both never averages one into the other."""
     batch = "_batch_kernel" in name or ("sim_kernel<2, 1" in name and ", true>" in name)
     if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name or "eval_prep_pair_batch_kernel" in name \
+            or "eval_prep_fin_batch_kernel" in name \
             or "eval_prep_batch_kernel" in name or "eval_prep_pair_f16_kernel" in name \
             or "eval_prep_pair_f16_batch_kernel" in name:
         r = "pack_gt_scores"
