@@ -578,7 +578,7 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
                                                     int64_t nb, int64_t cap_b, bool flat = false,
-                                                    const L2Planes l2 = L2Planes{}) {
+                                                    const L2Planes l2 = L2Planes{}, int ch = 1) {
   int64_t* pre;
   if constexpr (DYN_PRE) {
     extern __shared__ int64_t fix_dyn_pre[];
@@ -611,12 +611,18 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
     return gld(cand + nb + (xcd + G * k) * cap_b + (cc - pre[k]));
   };
   // the next pair's entry is loaded one pair ahead: in flight with this pair's row loads (as a dependent load
-  // at the top of each pair it added a round trip to every pair)
-  const int64_t c0 = (int64_t)(blockIdx.x / G) * nw + wave;
+  // at the top of each pair it added a round trip to every pair).  ch > 1: each wave walks runs of ch consecutive
+  // pairs (the tiled walk's lists hold a query's pairs of a super-bucket back to back: its row is then fetched
+  // once and re-read from the L2 by the same wave, whatever the skew between the waves)
+  const int64_t c0 = ((int64_t)(blockIdx.x / G) * nw + wave) * ch;
+  const int64_t jump = stride * ch - ch + 1;  // from a run's last pair to the wave's next run
   uint64_t u_next = entry(c0);
-  for (int64_t c = c0; c < total; c += stride) {
+  for (int64_t c = c0, e = 0; c < total;) {
     const uint64_t u = u_next;
-    u_next = entry(c + stride);
+    const bool in_run = e + 1 < ch;
+    c += in_run ? 1 : jump;
+    e = in_run ? e + 1 : 0;
+    u_next = entry(c);
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     uint32_t flags = (uint32_t)(u >> 62);

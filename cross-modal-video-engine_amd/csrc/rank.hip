@@ -267,6 +267,57 @@ __global__ __launch_bounds__(TSORT_NT) void tile_sort_scatter_kernel(const uint6
     if (u[r] != ~0ull) dst[lh[tsort_bin(u[r], shift)] + pos[r]] = u[r];
 }
 
+// one block per (super-bucket, query tile) bin after the scatter (hist[sb][.] then holds each bin's end): the bin's
+// entries sorted by query row (i & 255: the row within the tile) in LDS and written back in place, so a query's pairs
+// of the super-bucket lie back to back.  Bins over TSORT_BIN_MAX entries stay in arrival order (a slower walk, the
+// same counts).
+constexpr int TSORT_BIN_MAX = 8192;
+__global__ __launch_bounds__(256) void tile_sort_bins_kernel(const int* __restrict__ hist, int nbins, int64_t nsb,
+                                                             int64_t cap_sb, uint64_t* __restrict__ out) {
+  __shared__ uint64_t buf[TSORT_BIN_MAX];
+  __shared__ int cnt[256];
+  const int64_t sb = blockIdx.y;
+  const int b = blockIdx.x;
+  const int* h = hist + sb * nbins;
+  const int start = b ? h[b - 1] : 0, end = h[b];
+  const int n = end - start;
+  if (n <= 1 || n > TSORT_BIN_MAX) return;  // (block-uniform)
+  uint64_t* p = out + nsb + sb * cap_sb + start;
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const uint64_t u = p[e];
+    buf[e] = u;
+    atomicAdd(&cnt[u & 255], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 256 counts: 4 per lane + a wave scan
+    const int l = threadIdx.x;
+    int v[4], sum = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[r] = cnt[4 * l + r];
+      sum += v[r];
+    }
+    int incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (l >= o) incl += t;
+    }
+    int run = incl - sum;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      cnt[4 * l + r] = run;
+      run += v[r];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const uint64_t u = buf[e];
+    p[atomicAdd(&cnt[u & 255], 1)] = u;
+  }
+}
+
 // XCD-ordered re-score of the bucketed undecided pairs (fixup_walk, cmve_internal.h)
 template <typename TQ, typename TG, bool PF>
 __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw, int64_t ldq,
@@ -275,9 +326,9 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t nb, int64_t cap_b) {
+                                                    int64_t nb, int64_t cap_b, int ch) {
   fixup_walk<TQ, TG, PF, true, true>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb,
-                               cap_b);
+                                     cap_b, false, L2Planes{}, ch);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -294,7 +345,7 @@ static int env_int(const char* name, int dflt) {
 template <typename TQ, typename TG, bool PF>
 static void launch_fix(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, const double* row_sgt,
                        const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t nb,
-                       int64_t cap_b) {
+                       int64_t cap_b, int ch) {
   static const int bpx_env = env_int("CMVE_FIX_BPX", 0);
   static const int per_cu = [] {
     int n = 0;
@@ -308,15 +359,15 @@ static void launch_fix(hipStream_t stream, const cmve_rows_t* q, const cmve_rows
   const unsigned lds = (unsigned)(((nb + 7) / 8 + 1) * sizeof(int64_t));  // the walk's bucket prefix
   hipLaunchKernelGGL((fixup_kernel<TQ, TG, PF>), dim3(8u * (unsigned)bpx), dim3(256), lds, stream, (const TQ*)q->raw,
                      q->raw_ld, q->inv_norm, (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt,
-                     col_cnt, cand, nb, cap_b);
+                     col_cnt, cand, nb, cap_b, ch);
 }
 
 static int launch_fixup_walk(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, const double* row_sgt,
                              const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand,
-                             int64_t nb, int64_t cap_b) {
+                             int64_t nb, int64_t cap_b, int ch = 1) {
   static const bool pf = env_int("CMVE_FIX_PF", 0) != 0;
 #define FIX(TQ, TG, PF) \
-  launch_fix<TQ, TG, PF>(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b)
+  launch_fix<TQ, TG, PF>(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b, ch)
 #define FIX2(TQ, TG) \
   if (pf) FIX(TQ, TG, true); else FIX(TQ, TG, false)
   if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) FIX2(float, float);
@@ -364,10 +415,15 @@ int launch_fixup_tiled(hipStream_t stream, const cmve_rows_t* q, const cmve_rows
   hipLaunchKernelGGL(tile_sort_scan_kernel, dim3((unsigned)t.nsb), dim3(TSORT_NT), 0, stream, hist, t.nbins, scratch);
   hipLaunchKernelGGL(tile_sort_scatter_kernel, grid, dim3(TSORT_NT), 0, stream, cand, t.nb, t.cap_b, t.G, t.shift,
                      t.nbins, hist, t.nsb, scratch);
+  static const int ch = std::max(1, env_int("CMVE_FIX_RUN", 16));  // pairs per wave run (study knob)
+  static const bool bins = env_int("CMVE_FIX_BINSORT", 1) != 0;
+  if (bins && t.shift == 8)
+    hipLaunchKernelGGL(tile_sort_bins_kernel, dim3((unsigned)t.nbins, (unsigned)t.nsb), dim3(256), 0, stream, hist,
+                       t.nbins, t.nsb, t.G * t.cap_b, scratch);
   int st = check_launch("tile_sort");
   if (st) return st;
   (void)dirs;
-  return launch_fixup_walk(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, scratch, t.nsb, t.G * t.cap_b);
+  return launch_fixup_walk(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, scratch, t.nsb, t.G * t.cap_b, ch);
 }
 
 // ---- rank from a materialised error matrix (lower = better) ----
