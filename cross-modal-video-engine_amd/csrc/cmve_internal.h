@@ -91,11 +91,48 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
 // ---- wave reductions (xor butterfly: every lane ends with bit-identical sums) ----
+#if CMVE_STUDY_DPP
+// study build (-DCMVE_STUDY_DPP=1, loaded through CMVE_LIB): the butterfly on the VALU (lanes l ^ 32 / l ^ 16 by
+// v_permlane32_swap / v_permlane16_swap, l ^ 8 by a DPP row rotate, then the 8-lane half mirror and two quad
+// permutes); every lane ends with the same bits.  Measured (profiles/scripts/fixup_dpp.sh): C4 ranking 8.47 ->
+// 8.22 ms, gallery-shard fix-up 1.155 -> 1.125 ms, 1M fix-up unchanged, ranks unchanged -- not worth moving every
+// exact-score reduction (wave_sum_k, wave_dot64_x2, ...) to a new summation order, which they must share
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)b, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+  const bool low32 = (__lane_id() & 32) == 0, low16 = (__lane_id() & 16) == 0;
+  {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const uint32_t plo = low32 ? lo[1] : lo[0], phi = low32 ? hi[1] : hi[0];
+    v += __builtin_bit_cast(double, ((uint64_t)phi << 32) | plo);
+  }
+  {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const uint32_t plo = low16 ? lo[1] : lo[0], phi = low16 ? hi[1] : hi[0];
+    v += __builtin_bit_cast(double, ((uint64_t)phi << 32) | plo);
+  }
+  v += dpp_f64<0x128>(v);  // row_ror:8 (l ^ 8 within a row of 16)
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  return v;
+}
+#else
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+#endif
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
