@@ -2226,6 +2226,10 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   const bool inline_l2 = inline_l2_env >= 0 ? inline_l2_env == 1 : true;
+  static const bool l3_inline = [] {  // study knob: the level-3 pairs re-scored in the rank GEMM (no list for the finish)
+    const char* e = getenv("CMVE_EVAL_L3_INLINE");
+    return e && atoi(e) != 0;
+  }();
   const bool l2 = P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2;
   P.fix_launch = l2 && !inline_l2;
   if (l2) {
@@ -2237,7 +2241,7 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     a.g_lo16 = P.sg.lo16;
     a.q_el = P.sq.err_lo16;
     a.g_el = P.sg.err_lo16;
-    if (!P.fix_launch) {
+    if (!P.fix_launch && !l3_inline) {
       c.l3_count = (unsigned*)(base + w.l3);
       c.l3 = (uint64_t*)(base + w.l3 + 8);
       c.l3_cap = EVAL_L3_CAP;
