@@ -319,6 +319,19 @@ __global__ __launch_bounds__(256) void tile_sort_bins_kernel(const int* __restri
 }
 
 // XCD-ordered re-score of the bucketed undecided pairs (fixup_walk, cmve_internal.h)
+// two pairs per wave per step (fixup_walk2); ch is not used (always 1)
+template <typename TQ, typename TG, bool PF>
+__global__ __launch_bounds__(256) void fixup2_kernel(const TQ* __restrict__ qraw, int64_t ldq,
+                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
+                                                     int64_t ldg, const double* __restrict__ ginv, int64_t d,
+                                                     const double* __restrict__ row_sgt,
+                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
+                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
+                                                     int64_t nb, int64_t cap_b, int ch) {
+  (void)ch;
+  fixup_walk2<TQ, TG, PF>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b);
+}
+
 template <typename TQ, typename TG, bool PF>
 __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -347,19 +360,28 @@ static void launch_fix(hipStream_t stream, const cmve_rows_t* q, const cmve_rows
                        const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t nb,
                        int64_t cap_b, int ch) {
   static const int bpx_env = env_int("CMVE_FIX_BPX", 0);
-  static const int per_cu = [] {
+  static const bool x2 = env_int("CMVE_FIX_X2", 0) != 0 && ch == 1;
+  auto kern = x2 ? fixup2_kernel<TQ, TG, PF> : fixup_kernel<TQ, TG, PF>;
+  static const int per_cu1 = [] {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fixup_kernel<TQ, TG, PF>, 256, 512) != hipSuccess)
       n = 4;
     return std::max(1, n);
   }();
+  static const int per_cu2 = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fixup2_kernel<TQ, TG, PF>, 256, 512) != hipSuccess)
+      n = 4;
+    return std::max(1, n);
+  }();
+  const int per_cu = x2 ? per_cu2 : per_cu1;
   const int64_t row_bytes = q->d * std::max<int64_t>(sizeof(TQ), sizeof(TG));
   const int bpx = bpx_env > 0 ? std::min(1024, bpx_env)
                   : row_bytes < 4096 ? per_cu * std::max(1, device_cus() / 8) : 128;
   const unsigned lds = (unsigned)(((nb + 7) / 8 + 1) * sizeof(int64_t));  // the walk's bucket prefix
-  hipLaunchKernelGGL((fixup_kernel<TQ, TG, PF>), dim3(8u * (unsigned)bpx), dim3(256), lds, stream, (const TQ*)q->raw,
-                     q->raw_ld, q->inv_norm, (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt,
-                     col_cnt, cand, nb, cap_b, ch);
+  hipLaunchKernelGGL(kern, dim3(8u * (unsigned)bpx), dim3(256), lds, stream, (const TQ*)q->raw, q->raw_ld, q->inv_norm,
+                     (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb,
+                     cap_b, ch);
 }
 
 static int launch_fixup_walk(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, const double* row_sgt,
