@@ -2347,6 +2347,8 @@ struct cmve_eval_batch {
   hipEvent_t ev_in = nullptr, ev_prep = nullptr;  // cmve_eval_batch_run_split's stream hand-offs
   std::vector<void*> ws;          // the evaluations' workspaces (a chained run refuses a previous batch sharing one)
   bool chainable = false;         // the specialised paired prep: the chained run fuses it with the previous finish
+  bool pending = false;           // its last run was chained and its finish has not been enqueued yet ...
+  hipStream_t pending_stream = nullptr;  // ... on this stream (the next chained run there, or cmve_eval_batch_finish)
 };
 
 // the batch's rank geometry: 128 x 128 tiles on 4 waves of 64 x 64 (a 2-stage ring of 32 KiB stages, two blocks of
@@ -2558,6 +2560,8 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, 
 extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_slot) {
   CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run: NULL handle / batch");
   CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
+  CMVE_REQUIRE(!b->pending, "cmve_eval_batch_run: the batch's last chained run is not finished (chain it as the previous "
+                            "batch of the next chained run, or call cmve_eval_batch_finish)");
   return eval_batch_run(h, b, h->stream, timing_slot);
 }
 
@@ -2566,8 +2570,11 @@ extern "C" int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t b,
   CMVE_REQUIRE(h && b && b->d_items && b->d_args, "cmve_eval_batch_run_chained: NULL handle / batch");
   CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS,
                "cmve_eval_batch_run_chained: bad timing slot");
+  CMVE_REQUIRE(!b->pending, "cmve_eval_batch_run_chained: the batch's last chained run is not finished yet");
   if (prev) {
     CMVE_REQUIRE(prev->d_items && prev != b, "cmve_eval_batch_run_chained: the previous batch is destroyed or the batch itself");
+    CMVE_REQUIRE(prev->pending && prev->pending_stream == h->stream,
+                 "cmve_eval_batch_run_chained: the previous batch has no chained run awaiting its finish on this stream");
     CMVE_REQUIRE(prev->count == b->count && prev->nq_pad == b->nq_pad && prev->ng_pad == b->ng_pad &&
                      prev->sq0.n == b->sq0.n && prev->sg0.n == b->sg0.n && prev->qf == b->qf && prev->gf == b->gf &&
                      prev->mode == b->mode && prev->paired == b->paired && prev->chainable == b->chainable,
@@ -2577,18 +2584,29 @@ extern "C" int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t b,
                    "cmve_eval_batch_run_chained: the batch shares a workspace with the previous batch, whose finish "
                    "runs in the same launch as its prep");
   }
-  return eval_batch_run(h, b, h->stream, timing_slot, true, prev);
+  const int st = eval_batch_run(h, b, h->stream, timing_slot, true, prev);
+  if (st) return st;
+  if (prev) prev->pending = false;
+  b->pending = true;
+  b->pending_stream = h->stream;
+  return CMVE_OK;
 }
 
 extern "C" int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t b) {
   CMVE_REQUIRE(h && b && b->d_items, "cmve_eval_batch_finish: NULL handle / batch");
-  return cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, h->stream);
+  CMVE_REQUIRE(b->pending && b->pending_stream == h->stream,
+               "cmve_eval_batch_finish: the batch has no chained run awaiting its finish on this stream");
+  const int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, h->stream);
+  if (st) return st;
+  b->pending = false;
+  return CMVE_OK;
 }
 
 extern "C" int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t b, void* prep_stream, int32_t timing_slot) {
   CMVE_REQUIRE(h && b && b->d_items && b->d_args && prep_stream, "cmve_eval_batch_run_split: NULL argument");
   CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS,
                "cmve_eval_batch_run_split: bad timing slot");
+  CMVE_REQUIRE(!b->pending, "cmve_eval_batch_run_split: the batch's last chained run is not finished");
   return eval_batch_run(h, b, (hipStream_t)prep_stream, timing_slot);
 }
 

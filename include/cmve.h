@@ -471,7 +471,9 @@ int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t batch, void* pr
  * before (NULL: none); its outputs are complete once this call's first launch has run.  cmve_eval_batch_finish runs
  * a batch's deferred finish alone (after a stream's last chained run).  prev must have the batch's shapes and share
  * no workspace with it.  Results equal cmve_eval_batch_run's bit for bit; timing_slot records the launches
- * (cmve_eval_kernel_timing: prep (with the previous finish), rank GEMM, fix-up, 0). */
+ * (cmve_eval_kernel_timing: prep (with the previous finish), rank GEMM, fix-up, 0).  A batch whose chained run
+ * awaits its finish is refused by every run call until that finish is enqueued (as the prev of the next chained
+ * run on the same stream, or by cmve_eval_batch_finish on it); prev must be such a batch of h's stream. */
 int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t batch, cmve_eval_batch_t prev, int32_t timing_slot);
 int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t batch);
 /* a HIP stream restricted to the CUs set in mask (bit i of word i / 32 = CU i; hipExtStreamCreateWithCUMask) */

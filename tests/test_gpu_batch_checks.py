@@ -138,8 +138,11 @@ def test_rank_batch_chained_equals_run(golden, torch_cuda, per):
     ms = batches[2].kernel_timing(3)
     assert ms[0] > 0 and ms[1] > 0 and ms[3] == 0.0
     twin = engine.RankBatch(groups[0][0][:per], groups[0][1][:per])
+    twin.run_chained(None)
     with pytest.raises(RuntimeError, match="shares a workspace"):
         batches[0].run_chained(twin)
+    twin.finish()
+    torch.cuda.synchronize()
     for b in batches + [twin]:
         b.close()
 
@@ -170,9 +173,18 @@ def test_rank_batch_chained_general_prep(torch_cuda):
         torch.cuda.synchronize()
         ref.append([s.out.clone() for s in sess])
         bats.append((rb, sess))
-    bats[0][0].run_chained(None)
-    bats[1][0].run_chained(bats[0][0])
-    bats[1][0].finish()
+    b0, b1 = bats[0][0], bats[1][0]
+    b0.run_chained(None)
+    with pytest.raises(RuntimeError, match="not finished"):
+        b0.run()  # its finish is still pending
+    b1.run_chained(b0)
+    with pytest.raises(RuntimeError, match="no chained run awaiting"):
+        b0.finish()  # (finished inside b1's first launch)
+    with pytest.raises(RuntimeError, match="not finished"):
+        b1.run_chained(b0)  # b1's own chained run still awaits its finish
+    b1.finish()
+    with pytest.raises(RuntimeError, match="no chained run awaiting"):
+        b1.finish()
     torch.cuda.synchronize()
     for (rb, sess), rs in zip(bats, ref):
         for s, r in zip(sess, rs):
