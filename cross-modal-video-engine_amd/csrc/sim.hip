@@ -950,9 +950,9 @@ void sim_kernel(
                       if (s2[u] - E2 > t) { lds_add_u32_async(&lds_cc[lc], 1); fl &= ~2u; }
                       else if (s2[u] + E2 < t) fl &= ~2u;
                     }
-                    if (fl && a.l3) {  // level 3 in the finish (a returning atomic: only these few pairs pay it)
-                      const unsigned slot = gadd(a.l3_count, 1u);
-                      if (slot < (unsigned)a.l3_cap) {
+                    if (fl && a.l3_count) {  // level 3: counted (a returning atomic: only these few pairs pay it),
+                      const unsigned slot = gadd(a.l3_count, 1u);  // listed for the finish (batches) or, with no
+                      if (a.l3 && slot < (unsigned)a.l3_cap) {     // list (one evaluation), re-scored right here
                         gst(a.l3 + slot, (unsigned long long)qr[u] | ((unsigned long long)gc[u] << 31) |
                                              ((unsigned long long)fl << 62));
                         fl = 0u;
@@ -2226,10 +2226,15 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   const bool inline_l2 = inline_l2_env >= 0 ? inline_l2_env == 1 : true;
-  static const bool l3_inline = [] {  // study knob: the level-3 pairs re-scored in the rank GEMM (no list for the finish)
-    const char* e = getenv("CMVE_EVAL_L3_INLINE");
+  // level 3 of ONE evaluation (cmve_eval_ranks, its graphs): re-scored inside the rank GEMM (its ~4 pairs cost the
+  // GEMM ~0.7 us and spare the finish its fp64 round trip, 5.2 -> 4.4 us: 32.5 -> 31.4 us back to back); batches list
+  // them for the finish (in a chained run it rides in the next prep launch).  Both count them (out[12]).
+  // CMVE_EVAL_L3_LIST=1: the single evaluation lists them too (tests / studies)
+  static const bool l3_list_env = [] {
+    const char* e = getenv("CMVE_EVAL_L3_LIST");
     return e && atoi(e) != 0;
   }();
+  const bool l3_inline = !batch && !l3_list_env;
   const bool l2 = P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2;
   P.fix_launch = l2 && !inline_l2;
   if (l2) {
@@ -2241,12 +2246,12 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     a.g_lo16 = P.sg.lo16;
     a.q_el = P.sq.err_lo16;
     a.g_el = P.sg.err_lo16;
-    if (!P.fix_launch && !l3_inline) {
+    if (!P.fix_launch) {
       c.l3_count = (unsigned*)(base + w.l3);
       c.l3 = (uint64_t*)(base + w.l3 + 8);
-      c.l3_cap = EVAL_L3_CAP;
+      c.l3_cap = l3_inline ? 0 : EVAL_L3_CAP;  // (0: the finish re-scores nothing; its count still reaches out[12])
       a.l3_count = c.l3_count;
-      a.l3 = (unsigned long long*)c.l3;
+      a.l3 = l3_inline ? nullptr : (unsigned long long*)c.l3;
       a.l3_cap = c.l3_cap;
     }
   }

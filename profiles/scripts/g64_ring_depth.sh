@@ -8,7 +8,7 @@ A="--steps 4 --warmup 2 --no-shard-leg --no-extras --no-cpu-baseline --no-replay
 for cfg in "s4|0|" "s6|0|$R/scratch/libcmve_g64s6.so" "s8|0|$R/scratch/libcmve_g64s8.so" "s8i|1|$R/scratch/libcmve_g64s8.so" "s4i|1|" "s8b|0|$R/scratch/libcmve_g64s8.so" "s4b|0|"; do
   IFS='|' read n inl lib <<< "$cfg"
   if [ -n "$lib" ]; then export CMVE_LIB=$lib; else unset CMVE_LIB; fi
-  CMVE_EVAL_L3_INLINE=$inl timeout -k 10 200 python bench.py $A > $O/b_$n.json 2> $O/b_$n.err || { echo "$n failed"; tail -5 $O/b_$n.err; exit 1; }
+  CMVE_EVAL_L3_LIST=$((1 - inl)) timeout -k 10 200 python bench.py $A > $O/b_$n.json 2> $O/b_$n.err || { echo "$n failed"; tail -5 $O/b_$n.err; exit 1; }
   python3 -c "
 import json
 d=json.loads(open('$O/b_$n.json').read().strip().splitlines()[-1])
