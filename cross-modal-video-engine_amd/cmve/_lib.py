@@ -84,11 +84,8 @@ SIGNATURES = {
     "cmve_eval_batch_create": (C.c_int, [C.c_int32, _vp, _vp, C.c_int32, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp,
                                          _vp]),
     "cmve_eval_batch_run": (C.c_int, [_vp, _vp, C.c_int32]),
-    "cmve_eval_batch_run_split": (C.c_int, [_vp, _vp, _vp, C.c_int32]),
     "cmve_eval_batch_run_chained": (C.c_int, [_vp, _vp, _vp, C.c_int32]),
     "cmve_eval_batch_finish": (C.c_int, [_vp, _vp]),
-    "cmve_stream_create_cu_mask": (C.c_int, [_vp, C.c_int32, C.POINTER(_vp)]),
-    "cmve_stream_destroy": (C.c_int, [_vp]),
     "cmve_eval_batch_destroy": (C.c_int, [_vp]),
     "cmve_topk_dense_merge": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp]),
     "cmve_mha_absorbed": (C.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i64, _vp, _i64, _f64,
@@ -105,9 +102,6 @@ SIGNATURES = {
     "cmve_rank_mfma": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                                  _vp]),
     "cmve_rank_fixup": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
-    "cmve_rank_fixup_tiled": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
-                                        _i64, _i32]),
-    "cmve_rank_fixup_tiled_scratch": (C.c_int64, [_P(Rows), _P(Rows), _i64, _i32]),
     "cmve_rank_count_overlap": (C.c_int, [_vp, _P(Rows), _P(Rows), _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _i64, _vp, _i32]),
     "cmve_overlap_mfma_ms": (C.c_int, [_vp, _P(_f32), _P(_i32)]),
@@ -168,7 +162,7 @@ for _name, (_res, _args) in SIGNATURES.items():
     _fn.restype = _res
     _fn.argtypes = _args
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 if lib.cmve_abi_version() != ABI_VERSION:
     raise ImportError(f"libcmve.so ABI version {lib.cmve_abi_version()} != {ABI_VERSION}: rebuild it")
 

@@ -298,15 +298,6 @@ class RankWorkspace:
         self.cand = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
         self.count = torch.zeros(_lib.MAX_CHUNKS, dtype=torch.int64, device=device)
         self.chunks = 1
-        self.scratch = None  # the tiled fix-up's sorted copy (cmve_rank_fixup_tiled), allocated on first use
-
-    def tiled_scratch(self, q: "RowSet", g: "RowSet", group: int) -> torch.Tensor:
-        need = int(lib.cmve_rank_fixup_tiled_scratch(C.byref(q.desc), C.byref(g.desc), self.cap, int(group)))
-        if need < 0:
-            raise _lib.CmveError("cmve_rank_fixup_tiled_scratch: bad arguments")
-        if self.scratch is None or self.scratch.numel() < need:
-            self.scratch = torch.empty(need, dtype=torch.int64, device=self.device)
-        return self.scratch
 
     @property
     def cap(self):
@@ -336,12 +327,10 @@ def rank_thresholds(a: RowSet, b: RowSet, sgt: torch.Tensor, mode: int):
 
 
 def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: Optional[RankWorkspace] = None,
-                      row_cnt=None, col_cnt=None, events=None, chunks: int = 1, tiled: Optional[int] = None):
+                      row_cnt=None, col_cnt=None, events=None, chunks: int = 1):
     """Enqueue the fused rank count (no sync).  row/col = (sgt, thr_hi, thr_lo) or None.
     chunks > 1: cmve_rank_count_overlap -- the gallery in `chunks` pieces, each piece's fp64
     fix-up on the handle's auxiliary stream behind the next piece's MFMA pass.
-    tiled = G >= 0 (chunks == 1): the fix-up regroups the pairs by (G gallery buckets, query tile) first
-    (cmve_rank_fixup_tiled; G = 0 picks the group size), for lists with many pairs per query tile.
     events = (start, mid, end) torch.cuda.Event triple recorded around the MFMA pass and the
     fix-up (with chunks > 1 the two overlap: mid is recorded with end)."""
     dirs = (_lib.DIR_ROW if row is not None else 0) | (_lib.DIR_COL if col is not None else 0)
@@ -370,14 +359,8 @@ def rank_count_launch(q: RowSet, g: RowSet, mode: int, row=None, col=None, ws: O
           "cmve_rank_mfma")
     if events is not None:
         events[1].record()
-    if tiled is not None and tiled >= 0:
-        sc = ws.tiled_scratch(q, g, tiled)
-        check(lib.cmve_rank_fixup_tiled(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]),
-                                        _ptr(row_cnt), _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count),
-                                        _ptr(sc), sc.numel(), int(tiled)), "cmve_rank_fixup_tiled")
-    else:
-        check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(row_cnt),
-                                  _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)), "cmve_rank_fixup")
+    check(lib.cmve_rank_fixup(h, C.byref(q.desc), C.byref(g.desc), dirs, _ptr(r[0]), _ptr(c[0]), _ptr(row_cnt),
+                              _ptr(col_cnt), _ptr(ws.cand), ws.cap, _ptr(ws.count)), "cmve_rank_fixup")
     if events is not None:
         events[2].record()
     return row_cnt, col_cnt
@@ -677,13 +660,11 @@ class RankBatch:
         self.sessions, self.outs, self.stream = sessions, outs, stream
         self._h = stream_handle(s0.device, stream) if stream is not None else None
 
-    def run(self, timing_slot: int = -1, wait_current: bool = True, prep_stream=None):
+    def run(self, timing_slot: int = -1, wait_current: bool = True):
         """Enqueue the batch; ``timing_slot`` >= 0 records its launches' durations in that slot of the stream
         handle's timing ring (``kernel_timing``).  With a batch stream the run first waits for the work already
         enqueued on the caller's current stream (the producer that refilled the inputs, as RankSession.enqueue
-        does); ``wait_current=False`` skips that for inputs known to be complete.  ``prep_stream`` (a torch
-        stream): the prep launch goes there (``cmve_eval_batch_run_split``) -- e.g. a stream on CUs of its own,
-        ``cu_mask_stream``."""
+        does); ``wait_current=False`` skips that for inputs known to be complete."""
         if not self._b:
             raise RuntimeError("RankBatch.run: the batch was closed")
         if any(s._ws_gen != g for s, g in zip(self.sessions, self._ws_gens)):
@@ -693,11 +674,7 @@ class RankBatch:
             if cur.cuda_stream != self.stream.cuda_stream:
                 self.stream.wait_stream(cur)
         h = self._h if self._h is not None else handle(self.sessions[0].device)
-        if prep_stream is not None:
-            check(lib.cmve_eval_batch_run_split(h, self._b, C.c_void_p(prep_stream.cuda_stream), int(timing_slot)),
-                  "cmve_eval_batch_run_split")
-        else:
-            check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
+        check(lib.cmve_eval_batch_run(h, self._b, int(timing_slot)), "cmve_eval_batch_run")
 
     def run_chained(self, prev: Optional["RankBatch"] = None, timing_slot: int = -1, wait_current: bool = True):
         """Enqueue the batch with its finish (the words of its outputs: ranks, R@K) deferred to the next chained run on
@@ -937,42 +914,3 @@ def gt_positions_fused(a: RowSet, b: RowSet, lists, mode: int = _lib.SIM_F16):
         p += len(l)
     return out
 
-
-def cu_mask_stream(device, cus):
-    """A torch stream (ExternalStream over a HIP stream of libcmve.so's) whose kernels run only on the CUs in
-    ``cus`` (indices into the device's CUs, at least one: ``cmve_stream_create_cu_mask``).  Destroy it with
-    ``close_cu_mask_stream`` once every tensor recorded on it is freed (a RankSession on this stream records the
-    inputs it reads in place: the caching allocator records an event on the stream when such a tensor is freed,
-    so the stream must outlive them).  Never destroyed behind the caller's back: a stream still open at exit is
-    released with the process."""
-    import torch
-    dev = torch.device(device)
-    n = torch.cuda.get_device_properties(dev).multi_processor_count
-    cus = list(cus)
-    if not cus:  # an all-zero mask: the runtime rejects the stream's kernels or never schedules them
-        raise ValueError("cu_mask_stream: no CU given")
-    words = (n + 31) // 32
-    mask = (C.c_uint32 * words)()
-    for c in cus:
-        if not 0 <= c < n:
-            raise ValueError(f"cu_mask_stream: CU {c} outside 0..{n - 1}")
-        mask[c // 32] |= 1 << (c % 32)
-    ptr = C.c_void_p()
-    with torch.cuda.device(dev):
-        check(lib.cmve_stream_create_cu_mask(mask, words, C.byref(ptr)), "cmve_stream_create_cu_mask")
-    _CU_STREAMS.add(ptr.value)
-    return torch.cuda.ExternalStream(ptr.value, device=dev)
-
-
-_CU_STREAMS = set()  # HIP streams made by cu_mask_stream and not yet closed
-
-
-def close_cu_mask_stream(stream):
-    """Destroy a ``cu_mask_stream`` now (after synchronising it); later uses of the object are errors.  Free the
-    tensors recorded on the stream first (see cu_mask_stream)."""
-    p = stream.cuda_stream
-    if p not in _CU_STREAMS:
-        raise ValueError("close_cu_mask_stream: not a live cu_mask_stream")
-    stream.synchronize()
-    _CU_STREAMS.discard(p)
-    check(lib.cmve_stream_destroy(C.c_void_p(p)), "cmve_stream_destroy")

@@ -14,7 +14,6 @@ and recall@K = 100 * mean(rank <= K).
 """
 from __future__ import annotations
 
-import os
 from typing import List, Sequence
 
 import numpy as np
@@ -92,14 +91,6 @@ def _positions(index_names: Sequence, names: Sequence) -> np.ndarray:
 _WS = {}  # undecided-pair lists kept per device across validation passes (grown once, then reused)
 
 
-def _fix_group() -> int:
-    """-1 (default): the plain bucket walk of the undecided pairs.  G >= 0: the tiled walk (cmve_rank_fixup_tiled,
-    G gallery buckets per super-bucket, 0 = the library's choice), which regroups the pairs by query tile first.
-    Measured on the C4 ranking (30,364 x 44,493): the same 17-18 GB fetched and 0.5 ms slower, so it is a study
-    path."""
-    return int(os.environ.get("CMVE_CIRR_FIX_GROUP", "-1"))
-
-
 def cirr_target_ranks(predicted_features: torch.Tensor, index_pooled: torch.Tensor, index_names: Sequence,
                       reference_names: Sequence, target_names: Sequence) -> np.ndarray:
     """1-based rank of each query's target after removing its reference video; 0 = never retrieved.
@@ -125,7 +116,7 @@ def cirr_target_ranks(predicted_features: torch.Tensor, index_pooled: torch.Tens
     if ws is None or ws.cap < 64 * (q.n + g.n):
         ws = _WS[str(dev)] = engine.RankWorkspace(dev, cap=max(1 << 16, 64 * (q.n + g.n)))
     for _attempt in range(4):
-        cnt, _ = engine.rank_count_launch(q, g, mode, row=(s_t, hi, lo), ws=ws, tiled=_fix_group())
+        cnt, _ = engine.rank_count_launch(q, g, mode, row=(s_t, hi, lo), ws=ws)
         ncand = ws.ncand()
         if not ws.overflowed():
             break

@@ -91,48 +91,11 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
 // ---- wave reductions (xor butterfly: every lane ends with bit-identical sums) ----
-#if CMVE_STUDY_DPP
-// study build (-DCMVE_STUDY_DPP=1, loaded through CMVE_LIB): the butterfly on the VALU (lanes l ^ 32 / l ^ 16 by
-// v_permlane32_swap / v_permlane16_swap, l ^ 8 by a DPP row rotate, then the 8-lane half mirror and two quad
-// permutes); every lane ends with the same bits.  Measured (profiles/scripts/fixup_dpp.sh): C4 ranking 8.47 ->
-// 8.22 ms, gallery-shard fix-up 1.155 -> 1.125 ms, 1M fix-up unchanged, ranks unchanged -- not worth moving every
-// exact-score reduction (wave_sum_k, wave_dot64_x2, ...) to a new summation order, which they must share
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)b, CTRL, 0xf, 0xf, false);
-  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ double wave_sum(double v) {
-  const bool low32 = (__lane_id() & 32) == 0, low16 = (__lane_id() & 16) == 0;
-  {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
-    const uint32_t plo = low32 ? lo[1] : lo[0], phi = low32 ? hi[1] : hi[0];
-    v += __builtin_bit_cast(double, ((uint64_t)phi << 32) | plo);
-  }
-  {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
-    const uint32_t plo = low16 ? lo[1] : lo[0], phi = low16 ? hi[1] : hi[0];
-    v += __builtin_bit_cast(double, ((uint64_t)phi << 32) | plo);
-  }
-  v += dpp_f64<0x128>(v);  // row_ror:8 (l ^ 8 within a row of 16)
-  v += dpp_f64<0x141>(v);  // row_half_mirror
-  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
-  return v;
-}
-#else
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-#endif
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -291,70 +254,6 @@ __device__ __forceinline__ void wave_dot64_x2(const TA* __restrict__ a, const TB
       load4d(b2 + k, y2);
       fma4(acc, x, y);
       fma4(acc2, x2, y2);
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {  // wave_sum of both, interleaved
-      acc += __shfl_xor(acc, o, 64);
-      acc2 += __shfl_xor(acc2, o, 64);
-    }
-    s1 = acc;
-    s2 = acc2;
-    return;
-  }
-  s1 = wave_dot64(a, b, d, lane);
-  s2 = wave_dot64(a2, b2, d, lane);
-}
-
-// wave_dot64 of two pairs with the loads of both in flight two 256-element strides at a time, kept in their
-// storage type until their fma (fp32 rows: 4 registers per 16-B piece instead of 8), each chain in wave_dot64's
-// (m, c) order and the two butterflies interleaved: the same bits as two wave_dot64 calls, at a register budget
-// that leaves room for two pairs per wave in the fix-up walk
-template <typename T> struct Piece4;
-template <> struct Piece4<float> {
-  cmve_f32x4 v;
-  __device__ __forceinline__ void load(const float* p) { v = gld((const cmve_f32x4*)p); }
-  __device__ __forceinline__ double operator[](int c) const { return (double)v[c]; }
-};
-template <> struct Piece4<double> {
-  cmve_f64x2 a, b;
-  __device__ __forceinline__ void load(const double* p) {
-    a = gld((const cmve_f64x2*)p);
-    b = gld((const cmve_f64x2*)(p + 2));
-  }
-  __device__ __forceinline__ double operator[](int c) const { return c < 2 ? a[c] : b[c - 2]; }
-};
-template <typename TA, typename TB>
-__device__ __forceinline__ void wave_dot64_2l(const TA* __restrict__ a, const TB* __restrict__ b,
-                                              const TA* __restrict__ a2, const TB* __restrict__ b2, int64_t d,
-                                              int lane, double& s1, double& s2) {
-  if ((d & 3) == 0 && ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)a2) | ((uintptr_t)b2)) & 15) == 0) {
-    double acc = 0.0, acc2 = 0.0;
-    int64_t k = (int64_t)lane * 4;
-    for (; k < d; k += 512) {
-      const bool two = k + 256 < d;
-      Piece4<TA> x0, x1, z0, z1;
-      Piece4<TB> y0, y1, w0, w1;
-      x0.load(a + k);
-      y0.load(b + k);
-      z0.load(a2 + k);
-      w0.load(b2 + k);
-      if (two) {
-        x1.load(a + k + 256);
-        y1.load(b + k + 256);
-        z1.load(a2 + k + 256);
-        w1.load(b2 + k + 256);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc = fma(x0[c], y0[c], acc);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc2 = fma(z0[c], w0[c], acc2);
-      if (two) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc = fma(x1[c], y1[c], acc);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc2 = fma(z1[c], w1[c], acc2);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // (the next strides' loads stay below these fmas)
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {  // wave_sum of both, interleaved
@@ -679,7 +578,7 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
                                                     int64_t nb, int64_t cap_b, bool flat = false,
-                                                    const L2Planes l2 = L2Planes{}, int ch = 1) {
+                                                    const L2Planes l2 = L2Planes{}) {
   int64_t* pre;
   if constexpr (DYN_PRE) {
     extern __shared__ int64_t fix_dyn_pre[];
@@ -712,17 +611,12 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
     return gld(cand + nb + (xcd + G * k) * cap_b + (cc - pre[k]));
   };
   // the next pair's entry is loaded one pair ahead: in flight with this pair's row loads (as a dependent load
-  // at the top of each pair it added a round trip to every pair).  ch > 1: each wave walks runs of ch consecutive
-  // pairs (the tiled walk's lists hold a query's pairs of a super-bucket back to back: its row is then fetched
-  // once and re-read from the L2 by the same wave, whatever the skew between the waves)
-  const int64_t c0 = ((int64_t)(blockIdx.x / G) * nw + wave) * ch;
-  const int64_t jump = stride * ch - ch + 1;  // from a run's last pair to the wave's next run
+  // at the top of each pair it added a round trip to every pair)
+  const int64_t c0 = (int64_t)(blockIdx.x / G) * nw + wave;
   uint64_t u_next = entry(c0);
-  for (int64_t c = c0, e = 0; c < total;) {
+  for (int64_t c = c0; c < total;) {
     const uint64_t u = u_next;
-    const bool in_run = e + 1 < ch;
-    c += in_run ? 1 : jump;
-    e = in_run ? e + 1 : 0;
+    c += stride;
     u_next = entry(c);
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
@@ -759,70 +653,6 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
     if (lane == 0) {
       if ((flags & 1u) && row_sgt && s > (PREFETCH ? rs : gld(row_sgt + i))) gadd(row_cnt + i, 1);
       if ((flags & 2u) && col_sgt && s > (PREFETCH ? cs : gld(col_sgt + j))) gadd(col_cnt + j, 1);
-    }
-  }
-}
-
-// fixup_walk (plain form: no level-2 planes, dynamic LDS prefix, ch = 1) with TWO pairs per wave per step: pairs c
-// and c + 1 of the wave's step, every row load of both in flight (wave_dot64_2l), so a wave keeps two round trips in
-// flight instead of one -- the same scores, the same counts
-template <typename TQ, typename TG, bool PREFETCH>
-__device__ __forceinline__ void fixup_walk2(const TQ* __restrict__ qraw, int64_t ldq, const double* __restrict__ qinv,
-                                            const TG* __restrict__ graw, int64_t ldg, const double* __restrict__ ginv,
-                                            int64_t d, const double* __restrict__ row_sgt,
-                                            const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
-                                            int* __restrict__ col_cnt, const uint64_t* __restrict__ cand, int64_t nb,
-                                            int64_t cap_b) {
-  extern __shared__ int64_t fix_dyn_pre[];
-  int64_t* pre = fix_dyn_pre;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int G = 8;
-  const int xcd = blockIdx.x & 7;
-  const int64_t nk = xcd < nb ? (nb - xcd + G - 1) / G : 0;
-  if (wave == 0) fixup_prefix(cand, nb, cap_b, xcd, G, nk, lane, pre);
-  __syncthreads();
-  const int64_t total = pre[nk];
-  const int nw = (int)(blockDim.x >> 6);
-  const int64_t stride = (int64_t)(gridDim.x / G) * nw * 2;
-  int64_t k = 0;
-  auto entry = [&](int64_t cc) -> uint64_t {  // (as fixup_walk's; cc increases call by call)
-    if (cc >= total) return 0ull;
-    if (pre[k + 1] <= cc) {
-      int64_t lo = k + 1, hi = nk - 1;
-      while (lo < hi) {
-        const int64_t mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= cc) lo = mid;
-        else hi = mid - 1;
-      }
-      k = lo;
-    }
-    return gld(cand + nb + (xcd + G * k) * cap_b + (cc - pre[k]));
-  };
-  const int64_t c0 = ((int64_t)(blockIdx.x / G) * nw + wave) * 2;
-  uint64_t n1 = entry(c0), n2 = entry(c0 + 1);
-  for (int64_t c = c0; c < total; c += stride) {
-    const uint64_t u1 = n1, u2 = n2;
-    n1 = entry(c + stride);
-    n2 = entry(c + stride + 1);
-    const int64_t i1 = (int64_t)(u1 & 0x7fffffffull), j1 = (int64_t)((u1 >> 31) & 0x7fffffffull);
-    const int64_t i2 = (int64_t)(u2 & 0x7fffffffull), j2 = (int64_t)((u2 >> 31) & 0x7fffffffull);
-    const uint32_t f1 = (uint32_t)(u1 >> 62), f2 = (uint32_t)(u2 >> 62);  // (0: past the end, a null entry)
-    double rs1 = 0.0, cs1 = 0.0, rs2 = 0.0, cs2 = 0.0;
-    if (PREFETCH) {
-      rs1 = ((f1 & 1u) && row_sgt) ? gld(row_sgt + i1) : 0.0;
-      cs1 = ((f1 & 2u) && col_sgt) ? gld(col_sgt + j1) : 0.0;
-      rs2 = ((f2 & 1u) && row_sgt) ? gld(row_sgt + i2) : 0.0;
-      cs2 = ((f2 & 2u) && col_sgt) ? gld(col_sgt + j2) : 0.0;
-    }
-    const double sc1 = gld(qinv + i1) * gld(ginv + j1), sc2 = gld(qinv + i2) * gld(ginv + j2);
-    double d1, d2;
-    wave_dot64_2l(qraw + i1 * ldq, graw + j1 * ldg, qraw + i2 * ldq, graw + j2 * ldg, d, lane, d1, d2);
-    const double s1 = d1 * sc1, s2 = d2 * sc2;  // (wave_cos64's product order)
-    if (lane == 0) {
-      if ((f1 & 1u) && row_sgt && s1 > (PREFETCH ? rs1 : gld(row_sgt + i1))) gadd(row_cnt + i1, 1);
-      if ((f1 & 2u) && col_sgt && s1 > (PREFETCH ? cs1 : gld(col_sgt + j1))) gadd(col_cnt + j1, 1);
-      if ((f2 & 1u) && row_sgt && s2 > (PREFETCH ? rs2 : gld(row_sgt + i2))) gadd(row_cnt + i2, 1);
-      if ((f2 & 2u) && col_sgt && s2 > (PREFETCH ? cs2 : gld(col_sgt + j2))) gadd(col_cnt + j2, 1);
     }
   }
 }

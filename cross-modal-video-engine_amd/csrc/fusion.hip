@@ -655,18 +655,17 @@ extern "C" int cmve_mha_absorbed(cmve_handle_t h, const float* y, int64_t ldy, i
   if (B == 0) return CMVE_OK;
   const int cpr = (int)(d / npix), L = (int)(C / cpr);
   CMVE_REQUIRE(4 * npix * ldy < ((int64_t)1 << 31), "cmve_mha_absorbed: a key block's span exceeds 2 GiB");
-  static const int rows = [] {  // key rows per step (1, 2 or 4; study knob CMVE_MHA_ROWS)
-    const char* e = getenv("CMVE_MHA_ROWS");
-    const int r = e ? atoi(e) : 1;
-    return (r == 2 || r == 4) ? r : 1;
-  }();
+#ifndef CMVE_MHA_ROWS
+#define CMVE_MHA_ROWS 1  // key rows per step (1, 2 or 4; a study build's -D)
+#endif
+#ifndef CMVE_MHA_HPW
+#define CMVE_MHA_HPW 4  // heads per wave (4: two waves per query, 2: four; a study build's -D)
+#endif
+  constexpr int rows = (CMVE_MHA_ROWS == 2 || CMVE_MHA_ROWS == 4) ? CMVE_MHA_ROWS : 1;
   // (round 4, tools/ab_mha.sh at C4 size: 4 heads x 1 row 36.4 ms per combine_batches pass, 4 x 2 36.7, 2 x 1 37.9,
   // 2 x 2 37.8, 2 x 4 38.5 -- four waves read every key row twice as often, and more rows per step only add
   // registers: the kernel is not waiting on its loads)
-  static const int hpw = [] {  // heads per wave (4: two waves per query, 2: four; study knob CMVE_MHA_HPW)
-    const char* e = getenv("CMVE_MHA_HPW");
-    return (e && atoi(e) == 2) ? 2 : 4;
-  }();
+  constexpr int hpw = CMVE_MHA_HPW == 2 ? 2 : 4;
   const int T = (int)(f * L), R = (T % rows == 0) ? rows : ((T % 2 == 0) ? 2 : 1);
 #define CMVE_MHA_LAUNCH(E_, HW_, R_)                                                                                 \
   hipLaunchKernelGGL((mha_absorbed_kernel<E_, HW_, 8 / HW_, R_>), dim3((unsigned)B), dim3(64 * (8 / HW_)), 0,         \

@@ -127,211 +127,7 @@ int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* can
   return check_launch("cand_finalize");
 }
 
-// ---- tiled fix-up: the undecided pairs regrouped by (gallery super-bucket, query tile) before the walk ----
-// The rank GEMM fills a gallery bucket from ~32 query tiles at once, so the plain walk streams each pair's query
-// row from beyond the XCD's L2 (C4: 1.34 KB fetched per pair, 18 GB per pass).  Here G consecutive buckets form a
-// super-bucket whose gallery rows fit an XCD's L2 (G * 256 rows), and its pairs are counting-sorted by query
-// tile (i >> shift): the XCD's waves then walk one tile's pairs at a time, its 256 query rows reused across the
-// super-bucket's G * 256 gallery rows.  Three launches: per-chunk histograms into hist[sb][bin] (global adds),
-// an exclusive scan per super-bucket (the header count), a scatter reserving each chunk's range per bin.
-// The counts are integer increments: the order of the walk does not change them.
-constexpr int TSORT_NT = 1024;
-constexpr int TSORT_PER = 8;  // entries per thread and chunk
-constexpr int TSORT_CHUNK = TSORT_NT * TSORT_PER;
-constexpr int TSORT_MAX_BINS = 4096;
-
-struct TileSort {
-  int64_t nb, cap_b, nsb;  // buckets, their capacity, super-buckets
-  int G, shift, nbins;     // buckets per super-bucket, query-tile shift, bins per super-bucket
-};
-inline TileSort tile_sort_plan(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int group) {
-  const CandLayout l = cand_layout(g->n_pad, cand_cap);
-  TileSort t;
-  t.nb = l.nb;
-  t.cap_b = l.cap_b;
-  if (group <= 0) {  // the super-bucket's raw gallery rows within 2 MiB of the XCD's 4 MiB L2
-    const int64_t bucket_bytes = 256 * g->d * (g->raw_dtype == CMVE_F64 ? 8 : 4);
-    group = (int)std::max<int64_t>(1, std::min<int64_t>(8, (2ll << 20) / std::max<int64_t>(1, bucket_bytes)));
-  }
-  t.G = group;
-  t.nsb = (t.nb + t.G - 1) / t.G;
-  t.shift = 8;
-  while (((std::max<int64_t>(q->n_pad, 1) - 1) >> t.shift) + 1 > TSORT_MAX_BINS) ++t.shift;
-  t.nbins = (int)(((std::max<int64_t>(q->n_pad, 1) - 1) >> t.shift) + 1);
-  return t;
-}
-// scratch words: the sorted copy (header + regions, within cand_cap) and the int32 hist[nsb][nbins]
-inline int64_t tile_sort_scratch_words(const TileSort& t, int64_t cand_cap) {
-  return cand_cap + (t.nsb * t.nbins + 1) / 2;
-}
-
-__device__ __forceinline__ int tsort_bin(uint64_t u, int shift) { return (int)((u & 0x7fffffffull) >> shift); }
-
-// block (chunk c, bucket b): the chunk's entries, loaded TSORT_PER per thread ahead of their LDS adds
-__global__ __launch_bounds__(TSORT_NT) void tile_sort_hist_kernel(const uint64_t* __restrict__ cand, int64_t nb,
-                                                                  int64_t cap_b, int G, int shift, int nbins,
-                                                                  int* __restrict__ hist) {
-  __shared__ int lh[TSORT_MAX_BINS];
-  const int64_t b = blockIdx.y;
-  const int64_t n = min((int64_t)gld(cand + b), cap_b);
-  const int64_t e0 = (int64_t)blockIdx.x * TSORT_CHUNK;
-  if (e0 >= n) return;  // (block-uniform)
-  for (int k = threadIdx.x; k < nbins; k += TSORT_NT) lh[k] = 0;
-  __syncthreads();
-  const uint64_t* src = cand + nb + b * cap_b;
-  uint64_t u[TSORT_PER];
-#pragma unroll
-  for (int r = 0; r < TSORT_PER; ++r) {
-    const int64_t e = e0 + r * TSORT_NT + threadIdx.x;
-    u[r] = e < n ? gld(src + e) : ~0ull;
-  }
-#pragma unroll
-  for (int r = 0; r < TSORT_PER; ++r)
-    if (u[r] != ~0ull) atomicAdd(&lh[tsort_bin(u[r], shift)], 1);
-  __syncthreads();
-  int* gh = hist + (b / G) * nbins;
-  for (int k = threadIdx.x; k < nbins; k += TSORT_NT)
-    if (lh[k]) atomicAdd(gh + k, lh[k]);
-}
-
-// one block per super-bucket: hist[sb][.] -> its exclusive prefix (the scatter's cursors); out[sb] = the total
-__global__ __launch_bounds__(TSORT_NT) void tile_sort_scan_kernel(int* __restrict__ hist, int nbins,
-                                                                  uint64_t* __restrict__ out) {
-  __shared__ int wsum[TSORT_NT / 64];
-  int* h = hist + (int64_t)blockIdx.x * nbins;
-  const int per = (nbins + TSORT_NT - 1) / TSORT_NT;  // <= 4
-  const int k0 = threadIdx.x * per;
-  int v[4], sum = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = (r < per && k0 + r < nbins) ? h[k0 + r] : 0;
-    sum += v[r];
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int incl = sum;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int before = 0, total = 0;
-  for (int k = 0; k < TSORT_NT / 64; ++k) {
-    before += k < w ? wsum[k] : 0;
-    total += wsum[k];
-  }
-  int run = before + incl - sum;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (r < per && k0 + r < nbins) {
-      h[k0 + r] = run;
-      run += v[r];
-    }
-  if (threadIdx.x == 0) out[blockIdx.x] = (uint64_t)total;
-}
-
-// block (chunk c, bucket b): rank of each entry within its bin in this chunk (LDS adds), one returning global add
-// per non-empty bin reserves the chunk's range, then the entries land at nsb + sb * G * cap_b + cursor
-__global__ __launch_bounds__(TSORT_NT) void tile_sort_scatter_kernel(const uint64_t* __restrict__ cand, int64_t nb,
-                                                                     int64_t cap_b, int G, int shift, int nbins,
-                                                                     int* __restrict__ hist, int64_t nsb,
-                                                                     uint64_t* __restrict__ out) {
-  __shared__ int lh[TSORT_MAX_BINS];
-  const int64_t b = blockIdx.y;
-  const int64_t n = min((int64_t)gld(cand + b), cap_b);
-  const int64_t e0 = (int64_t)blockIdx.x * TSORT_CHUNK;
-  if (e0 >= n) return;
-  for (int k = threadIdx.x; k < nbins; k += TSORT_NT) lh[k] = 0;
-  __syncthreads();
-  const uint64_t* src = cand + nb + b * cap_b;
-  uint64_t u[TSORT_PER];
-  int pos[TSORT_PER];
-#pragma unroll
-  for (int r = 0; r < TSORT_PER; ++r) {
-    const int64_t e = e0 + r * TSORT_NT + threadIdx.x;
-    u[r] = e < n ? gld(src + e) : ~0ull;
-  }
-#pragma unroll
-  for (int r = 0; r < TSORT_PER; ++r) pos[r] = u[r] != ~0ull ? atomicAdd(&lh[tsort_bin(u[r], shift)], 1) : 0;
-  __syncthreads();
-  const int64_t sb = b / G;
-  int* gh = hist + sb * nbins;
-  for (int k = threadIdx.x; k < nbins; k += TSORT_NT) {
-    const int c = lh[k];
-    if (c) lh[k] = atomicAdd(gh + k, c);  // (each bin is read and rewritten by one thread)
-  }
-  __syncthreads();
-  uint64_t* dst = out + nsb + sb * G * cap_b;
-#pragma unroll
-  for (int r = 0; r < TSORT_PER; ++r)
-    if (u[r] != ~0ull) dst[lh[tsort_bin(u[r], shift)] + pos[r]] = u[r];
-}
-
-// one block per (super-bucket, query tile) bin after the scatter (hist[sb][.] then holds each bin's end): the bin's
-// entries sorted by query row (i & 255: the row within the tile) in LDS and written back in place, so a query's pairs
-// of the super-bucket lie back to back.  Bins over TSORT_BIN_MAX entries stay in arrival order (a slower walk, the
-// same counts).
-constexpr int TSORT_BIN_MAX = 8192;
-__global__ __launch_bounds__(256) void tile_sort_bins_kernel(const int* __restrict__ hist, int nbins, int64_t nsb,
-                                                             int64_t cap_sb, uint64_t* __restrict__ out) {
-  __shared__ uint64_t buf[TSORT_BIN_MAX];
-  __shared__ int cnt[256];
-  const int64_t sb = blockIdx.y;
-  const int b = blockIdx.x;
-  const int* h = hist + sb * nbins;
-  const int start = b ? h[b - 1] : 0, end = h[b];
-  const int n = end - start;
-  if (n <= 1 || n > TSORT_BIN_MAX) return;  // (block-uniform)
-  uint64_t* p = out + nsb + sb * cap_sb + start;
-  cnt[threadIdx.x] = 0;
-  __syncthreads();
-  for (int e = threadIdx.x; e < n; e += 256) {
-    const uint64_t u = p[e];
-    buf[e] = u;
-    atomicAdd(&cnt[u & 255], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {  // exclusive scan of the 256 counts: 4 per lane + a wave scan
-    const int l = threadIdx.x;
-    int v[4], sum = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[r] = cnt[4 * l + r];
-      sum += v[r];
-    }
-    int incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, o, 64);
-      if (l >= o) incl += t;
-    }
-    int run = incl - sum;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      cnt[4 * l + r] = run;
-      run += v[r];
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < n; e += 256) {
-    const uint64_t u = buf[e];
-    p[atomicAdd(&cnt[u & 255], 1)] = u;
-  }
-}
-
 // XCD-ordered re-score of the bucketed undecided pairs (fixup_walk, cmve_internal.h)
-// two pairs per wave per step (fixup_walk2); ch is not used (always 1)
-template <typename TQ, typename TG, bool PF>
-__global__ __launch_bounds__(256) void fixup2_kernel(const TQ* __restrict__ qraw, int64_t ldq,
-                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
-                                                     int64_t ldg, const double* __restrict__ ginv, int64_t d,
-                                                     const double* __restrict__ row_sgt,
-                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
-                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                     int64_t nb, int64_t cap_b, int ch) {
-  (void)ch;
-  fixup_walk2<TQ, TG, PF>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b);
-}
-
 template <typename TQ, typename TG, bool PF>
 __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw, int64_t ldq,
                                                     const double* __restrict__ qinv, const TG* __restrict__ graw,
@@ -339,14 +135,9 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t nb, int64_t cap_b, int ch) {
+                                                    int64_t nb, int64_t cap_b) {
   fixup_walk<TQ, TG, PF, true, true>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb,
-                                     cap_b, false, L2Planes{}, ch);
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
+                                     cap_b, false, L2Planes{});
 }
 
 // the walk over nb buckets of cap_b entries at cand (counts at cand[0, nb)).  Every wave has one pair in flight.
@@ -354,49 +145,41 @@ static int env_int(const char* name, int dflt) {
 // walk is bound by the round trips in flight there (C4 ranking 10.1 -> 8.5 ms; it used to be held to 16 waves per
 // CU by a 32 KiB static LDS prefix).  Wider rows (the 1024-d gallery shards: a query row per pair from the
 // Infinity Cache at ~6 TB/s) keep 128 blocks per XCD: more waves in flight only contend (1M-gallery fix-up 11.6 ->
-// 13.4 ms).  CMVE_FIX_BPX (blocks per XCD) and CMVE_FIX_PF (GT scores loaded ahead of the dot) are study knobs.
+// 13.4 ms).  Study builds: CMVE_FIX_BPX (blocks per XCD), CMVE_FIX_PF=1 (GT scores loaded ahead of the dot).
+#ifndef CMVE_FIX_BPX
+#define CMVE_FIX_BPX 0
+#endif
+#ifndef CMVE_FIX_PF
+#define CMVE_FIX_PF 0
+#endif
 template <typename TQ, typename TG, bool PF>
 static void launch_fix(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, const double* row_sgt,
                        const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t nb,
-                       int64_t cap_b, int ch) {
-  static const int bpx_env = env_int("CMVE_FIX_BPX", 0);
-  static const bool x2 = env_int("CMVE_FIX_X2", 0) != 0 && ch == 1;
-  auto kern = x2 ? fixup2_kernel<TQ, TG, PF> : fixup_kernel<TQ, TG, PF>;
-  static const int per_cu1 = [] {
+                       int64_t cap_b) {
+  static const int per_cu = [] {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fixup_kernel<TQ, TG, PF>, 256, 512) != hipSuccess)
       n = 4;
     return std::max(1, n);
   }();
-  static const int per_cu2 = [] {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fixup2_kernel<TQ, TG, PF>, 256, 512) != hipSuccess)
-      n = 4;
-    return std::max(1, n);
-  }();
-  const int per_cu = x2 ? per_cu2 : per_cu1;
   const int64_t row_bytes = q->d * std::max<int64_t>(sizeof(TQ), sizeof(TG));
-  const int bpx = bpx_env > 0 ? std::min(1024, bpx_env)
+  const int bpx = CMVE_FIX_BPX > 0 ? std::min(1024, CMVE_FIX_BPX)
                   : row_bytes < 4096 ? per_cu * std::max(1, device_cus() / 8) : 128;
   const unsigned lds = (unsigned)(((nb + 7) / 8 + 1) * sizeof(int64_t));  // the walk's bucket prefix
-  hipLaunchKernelGGL(kern, dim3(8u * (unsigned)bpx), dim3(256), lds, stream, (const TQ*)q->raw, q->raw_ld, q->inv_norm,
-                     (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb,
-                     cap_b, ch);
+  hipLaunchKernelGGL((fixup_kernel<TQ, TG, PF>), dim3(8u * (unsigned)bpx), dim3(256), lds, stream, (const TQ*)q->raw,
+                     q->raw_ld, q->inv_norm, (const TG*)g->raw, g->raw_ld, g->inv_norm, q->d, row_sgt, col_sgt, row_cnt,
+                     col_cnt, cand, nb, cap_b);
 }
 
 static int launch_fixup_walk(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, const double* row_sgt,
                              const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand,
-                             int64_t nb, int64_t cap_b, int ch = 1) {
-  static const bool pf = env_int("CMVE_FIX_PF", 0) != 0;
-#define FIX(TQ, TG, PF) \
-  launch_fix<TQ, TG, PF>(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b, ch)
-#define FIX2(TQ, TG) \
-  if (pf) FIX(TQ, TG, true); else FIX(TQ, TG, false)
-  if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) FIX2(float, float);
-  else if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F64) FIX2(float, double);
-  else if (q->raw_dtype == CMVE_F64 && g->raw_dtype == CMVE_F32) FIX2(double, float);
-  else FIX2(double, double);
-#undef FIX2
+                             int64_t nb, int64_t cap_b) {
+  constexpr bool PF = CMVE_FIX_PF != 0;
+#define FIX(TQ, TG) launch_fix<TQ, TG, PF>(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb, cap_b)
+  if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F32) FIX(float, float);
+  else if (q->raw_dtype == CMVE_F32 && g->raw_dtype == CMVE_F64) FIX(float, double);
+  else if (q->raw_dtype == CMVE_F64 && g->raw_dtype == CMVE_F32) FIX(double, float);
+  else FIX(double, double);
 #undef FIX
   return check_launch("fixup_kernel");
 }
@@ -412,40 +195,6 @@ int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g,
   // a disabled direction has flags that never set its bit; pass its (possibly NULL) arrays through
   (void)dirs;
   return launch_fixup_walk(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, cand, l.nb, l.cap_b);
-}
-
-int64_t fixup_tiled_scratch_words(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int group) {
-  return tile_sort_scratch_words(tile_sort_plan(q, g, cand_cap, group), cand_cap);
-}
-
-int launch_fixup_tiled(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
-                       const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
-                       const uint64_t* cand, int64_t cand_cap, uint64_t* scratch, int64_t scratch_cap, int group) {
-  const TileSort t = tile_sort_plan(q, g, cand_cap, group);
-  if (t.cap_b == 0) return CMVE_OK;  // reported as overflow by the MFMA pass: the caller retries
-  CMVE_REQUIRE(scratch_cap >= tile_sort_scratch_words(t, cand_cap),
-               "cmve_rank_fixup_tiled: scratch holds %lld words, needs %lld", (long long)scratch_cap,
-               (long long)tile_sort_scratch_words(t, cand_cap));
-  CMVE_REQUIRE(t.G * t.cap_b < (1ll << 31), "cmve_rank_fixup_tiled: super-bucket capacity exceeds 2^31 pairs");
-  CMVE_REQUIRE((t.nsb + 7) / 8 <= FIXUP_MAX_BUCKETS_PER_XCD,
-               "cmve_rank_fixup_tiled: gallery set too large (%lld super-buckets)", (long long)t.nsb);
-  int* hist = (int*)(scratch + cand_cap);
-  CMVE_HIP(hipMemsetAsync(hist, 0, sizeof(int) * t.nsb * t.nbins, stream));
-  const dim3 grid((unsigned)((t.cap_b + TSORT_CHUNK - 1) / TSORT_CHUNK), (unsigned)t.nb);
-  hipLaunchKernelGGL(tile_sort_hist_kernel, grid, dim3(TSORT_NT), 0, stream, cand, t.nb, t.cap_b, t.G, t.shift,
-                     t.nbins, hist);
-  hipLaunchKernelGGL(tile_sort_scan_kernel, dim3((unsigned)t.nsb), dim3(TSORT_NT), 0, stream, hist, t.nbins, scratch);
-  hipLaunchKernelGGL(tile_sort_scatter_kernel, grid, dim3(TSORT_NT), 0, stream, cand, t.nb, t.cap_b, t.G, t.shift,
-                     t.nbins, hist, t.nsb, scratch);
-  static const int ch = std::max(1, env_int("CMVE_FIX_RUN", 16));  // pairs per wave run (study knob)
-  static const bool bins = env_int("CMVE_FIX_BINSORT", 1) != 0;
-  if (bins && t.shift == 8)
-    hipLaunchKernelGGL(tile_sort_bins_kernel, dim3((unsigned)t.nbins, (unsigned)t.nsb), dim3(256), 0, stream, hist,
-                       t.nbins, t.nsb, t.G * t.cap_b, scratch);
-  int st = check_launch("tile_sort");
-  if (st) return st;
-  (void)dirs;
-  return launch_fixup_walk(stream, q, g, row_sgt, col_sgt, row_cnt, col_cnt, scratch, t.nsb, t.G * t.cap_b, ch);
 }
 
 // ---- rank from a materialised error matrix (lower = better) ----

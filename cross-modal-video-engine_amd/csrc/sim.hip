@@ -26,6 +26,29 @@
 
 #include "cmve_internal.h"
 
+// Study knobs are compile-time only (make study NAME=x DEFS="-D..."): the product build reads no environment.
+#ifndef CMVE_SIM_GN
+#define CMVE_SIM_GN 8  // gallery tiles per tile-order group (GN = 2..16 measured within 2%)
+#endif
+#ifndef CMVE_SIM_GEO
+#define CMVE_SIM_GEO 0  // 128: force G128; 2562: the 2-stage G256 loop
+#endif
+#ifndef CMVE_BATCH_GEO
+#define CMVE_BATCH_GEO 0  // K14 batch rank tile: 1288 / 256128 / 64 / 12864 (see batch_geo_force)
+#endif
+#ifndef CMVE_EVAL_DBG
+#define CMVE_EVAL_DBG 0  // K14 kernel studies: skip parts (results garbage) / 128: per-block stamps
+#endif
+#ifndef CMVE_EVAL_INLINE_L2
+#define CMVE_EVAL_INLINE_L2 1  // 0: the level-2 re-score in a fix-up launch instead of inside the rank GEMM
+#endif
+#ifndef CMVE_EVAL_NO_L2
+#define CMVE_EVAL_NO_L2 0  // 1: every band pair in fp64 inside the GEMM (no residual plane)
+#endif
+#ifndef CMVE_EVAL_L3_LIST
+#define CMVE_EVAL_L3_LIST 0  // 1: one evaluation lists its level-3 pairs for the finish as batches do
+#endif
+
 namespace cmve {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -1557,11 +1580,7 @@ void sim_kernel(
 static void geo_fill(SimArgs& a, int64_t nq_pad, int64_t ng_pad, int bm, int bn) {
   a.nblk_m = (int)(nq_pad / bm);
   a.nblk_n = (int)(ng_pad / bn);
-  static const int gn_env = [] {
-    const char* e = getenv("CMVE_SIM_GN");  // kernel studies only
-    return e ? atoi(e) : 0;
-  }();
-  a.gn = gn_env > 0 ? gn_env : 8;
+  a.gn = CMVE_SIM_GN;
 }
 
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
@@ -1584,15 +1603,9 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
 }
 
 // G256 (phased schedule) for bf16/fp16 when both sides tile by 256 and the grid has >= 512
-// tiles; G64 below 128 tiles of 128^2; else G128 (2-stage).  CMVE_SIM_GEO=128 / 2562 force G128 / the 2-stage G256 loop
-// (kernel studies only).
-static int sim_geo_force() {
-  static const int force = [] {
-    const char* e = getenv("CMVE_SIM_GEO");
-    return e ? atoi(e) : 0;
-  }();
-  return force;
-}
+// tiles; G64 below 128 tiles of 128^2; else G128 (2-stage).  Study builds (make study DEFS=-DCMVE_SIM_GEO=128 / 2562)
+// force G128 / the 2-stage G256 loop; the product build reads no environment.
+static constexpr int sim_geo_force() { return CMVE_SIM_GEO; }
 
 // true when launch_sim takes the persistent phased G256 kernel (which reads explicit thresholds only)
 static bool sim_uses_phased(int mode, int64_t nq_pad, int64_t ng_pad) {
@@ -1693,10 +1706,6 @@ int launch_cand_finalize(hipStream_t stream, const cmve_rows_t* g, uint64_t* can
 int launch_fixup(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs, const double* row_sgt,
                  const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt, const uint64_t* cand, int64_t cand_cap,
                  const int64_t* cand_count);
-int64_t fixup_tiled_scratch_words(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int group);
-int launch_fixup_tiled(hipStream_t stream, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
-                       const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
-                       const uint64_t* cand, int64_t cand_cap, uint64_t* scratch, int64_t scratch_cap, int group);
 }
 
 // point the epilogue at the bucketed layout of `cand` (cand_layout) for the gallery view g
@@ -1793,28 +1802,6 @@ extern "C" int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve
   if (q->n == 0 || g->n == 0) return CMVE_OK;  // nothing to re-score (an empty gallery shard)
   CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup: raw rows / norms missing");
   return launch_fixup(h->stream, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, cand_count);
-}
-
-extern "C" int64_t cmve_rank_fixup_tiled_scratch(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap,
-                                                 int32_t group) {
-  if (!q || !g || cand_cap < 0) return -1;
-  return fixup_tiled_scratch_words(q, g, cand_cap, group);
-}
-
-extern "C" int cmve_rank_fixup_tiled(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
-                                     const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
-                                     const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count,
-                                     uint64_t* scratch, int64_t scratch_cap, int32_t group) {
-  CMVE_REQUIRE(h && q && g, "cmve_rank_fixup_tiled: NULL argument");
-  CMVE_REQUIRE(q->d == g->d, "cmve_rank_fixup_tiled: dimension mismatch");
-  if (dirs & CMVE_DIR_ROW) CMVE_REQUIRE(row_sgt && row_cnt, "cmve_rank_fixup_tiled: row arrays missing");
-  if (dirs & CMVE_DIR_COL) CMVE_REQUIRE(col_sgt && col_cnt, "cmve_rank_fixup_tiled: col arrays missing");
-  CMVE_REQUIRE(cand && cand_count && scratch, "cmve_rank_fixup_tiled: candidate / scratch buffer missing");
-  CMVE_REQUIRE(group >= 0 && group <= 64, "cmve_rank_fixup_tiled: group must be 0 (auto) .. 64");
-  if (q->n == 0 || g->n == 0) return CMVE_OK;
-  CMVE_REQUIRE(q->raw && g->raw && q->inv_norm && g->inv_norm, "cmve_rank_fixup_tiled: raw rows / norms missing");
-  return launch_fixup_tiled(h->stream, q, g, dirs, row_sgt, col_sgt, row_cnt, col_cnt, cand, cand_cap, scratch,
-                            scratch_cap, group);
 }
 
 extern "C" int cmve_rank_count(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t mode, int32_t dirs,
@@ -2155,10 +2142,7 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   c.cap_b = l.cap_b;
   c.cand = cand;
   c.stats = out;
-  static const int dbg = [] {
-    const char* e = getenv("CMVE_EVAL_DBG");  // kernel studies only
-    return e ? atoi(e) : 0;
-  }();
+  constexpr int dbg = CMVE_EVAL_DBG;  // kernel studies only (a study build)
   c.dbg = dbg;
   static unsigned long long* stamp_buf = nullptr;
   if ((dbg & 128) && !stamp_buf) {
@@ -2206,9 +2190,7 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
     a.col_gt1 = P.sg.gt1;
   }
   // G64 (1k-A scale): the rank GEMM re-scores its own undecided pairs (no list, no fix-up launch)
-  const char* fix_env = getenv("CMVE_EVAL_FIX_LAUNCH");  // kernel studies / tests: the separate fix-up launch
-  const bool no_inline = fix_env && atoi(fix_env) != 0;
-  P.inline_fix = a.thr_gt && !no_inline && sim_uses_g64(q->n_pad, g->n_pad);
+  P.inline_fix = a.thr_gt && sim_uses_g64(q->n_pad, g->n_pad);
   // level-2 re-score from the fp16 + bf16 residual planes: the F16 mode whose prep runs the register path (the
   // only one that writes lo16: 16-B row pieces, d_pad <= 1024, both sides).  Two forms: (a) inline (the default)
   // -- level 2 inside the rank GEMM, level 3 deferred to the finish through the workspace's list; (b) the fix-up
@@ -2216,25 +2198,14 @@ static int eval_prepare(cmve_rows_t* q, cmve_rows_t* g, int32_t mode_flags, cons
   // re-scores them, two pairs per wave.  Measured (round 4, tools/ab_env.sh, batches of 8): (b) takes the round
   // trips out of the GEMM (38 -> 27 us) but its own launch costs 27 us -- its gathers miss the L2 the GEMM's
   // tiles had just filled -- and a single evaluation pays a launch boundary (b2b 35.0 vs 35.9 us).
-  // CMVE_EVAL_NO_L2 (tests / kernel studies): every band pair in fp64 inside the GEMM
-  static const bool no_l2 = [] {
-    const char* e = getenv("CMVE_EVAL_NO_L2");
-    return e && atoi(e) != 0;
-  }();
-  static const int inline_l2_env = [] {  // -1: the per-path default
-    const char* e = getenv("CMVE_EVAL_INLINE_L2");
-    return (e && *e) ? (atoi(e) != 0 ? 1 : 0) : -1;
-  }();
-  const bool inline_l2 = inline_l2_env >= 0 ? inline_l2_env == 1 : true;
+  // Study builds: CMVE_EVAL_INLINE_L2=0 (form b), CMVE_EVAL_NO_L2=1 (every band pair in fp64 inside the GEMM)
+  constexpr bool no_l2 = CMVE_EVAL_NO_L2 != 0;
+  constexpr bool inline_l2 = CMVE_EVAL_INLINE_L2 != 0;
   // level 3 of ONE evaluation (cmve_eval_ranks, its graphs): re-scored inside the rank GEMM (its ~4 pairs cost the
   // GEMM ~0.7 us and spare the finish its fp64 round trip, 5.2 -> 4.4 us: 32.5 -> 31.4 us back to back); batches list
   // them for the finish (in a chained run it rides in the next prep launch).  Both count them (out[12]).
-  // CMVE_EVAL_L3_LIST=1: the single evaluation lists them too (tests / studies)
-  static const bool l3_list_env = [] {
-    const char* e = getenv("CMVE_EVAL_L3_LIST");
-    return e && atoi(e) != 0;
-  }();
-  const bool l3_inline = !batch && !l3_list_env;
+  // Study builds: CMVE_EVAL_L3_LIST=1, the single evaluation lists them too
+  const bool l3_inline = !batch && CMVE_EVAL_L3_LIST == 0;
   const bool l2 = P.inline_fix && mode == CMVE_SIM_F16 && P.sq.vec && P.sg.vec && q->d_pad <= 1024 && !no_l2;
   P.fix_launch = l2 && !inline_l2;
   if (l2) {
@@ -2349,8 +2320,8 @@ struct cmve_eval_batch {
   bool fix_launch = false;        // the rank GEMM lists its undecided pairs for a fix-up launch
   cmve::EvalItem* d_items = nullptr;
   SimArgs* d_args = nullptr;
-  hipEvent_t ev_in = nullptr, ev_prep = nullptr;  // cmve_eval_batch_run_split's stream hand-offs
-  std::vector<void*> ws;          // the evaluations' workspaces (a chained run refuses a previous batch sharing one)
+  std::vector<void*> ws;          // the evaluations' workspaces and outputs: a chained run refuses a previous batch
+  std::vector<void*> outs;        // sharing either (its finish runs in the same launch as this batch's prep)
   bool chainable = false;         // the specialised paired prep: the chained run fuses it with the previous finish
   bool pending = false;           // its last run was chained and its finish has not been enqueued yet ...
   hipStream_t pending_stream = nullptr;  // ... on this stream (the next chained run there, or cmve_eval_batch_finish)
@@ -2363,13 +2334,7 @@ struct cmve_eval_batch {
 // it is slower (42 vs 36 us per batch of 8), beside the preps the headline gains 4-5% (1.18 vs 1.13e11 pairs/s,
 // round 5).  Split-bf16 (whose ring holds both planes) takes 128 x 64; kernel studies: CMVE_BATCH_GEO = 1288 (the
 // 8-wave 128 x 128), 256128 (256 x 128, one block per CU), 64 / 12864 (64 x 64 / 128 x 64).
-static int batch_geo_force() {
-  static const int force = [] {
-    const char* e = getenv("CMVE_BATCH_GEO");
-    return e ? atoi(e) : 0;
-  }();
-  return force;
-}
+static constexpr int batch_geo_force() { return CMVE_BATCH_GEO; }
 static bool batch_geo_big(int64_t nq_pad, int64_t ng_pad, int mode) {
   return batch_geo_force() == 256128 && nq_pad % 256 == 0 && ng_pad % 128 == 0 && mode != CMVE_SIM_BF16X3;
 }
@@ -2476,7 +2441,10 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
   b->c0 = P0.c;
   b->fix_launch = P0.fix_launch;
   b->ws.assign(ws, ws + count);
-  b->chainable = cmve::eval_batch_chainable(P0.sq, P0.sg, P0.c);
+  b->outs.assign(out, out + count);
+  // the fused chained launch runs the specialised PAIRED prep: a batch whose lists are no one-to-one pairing (run()
+  // takes the general prep, phase 0) chains through the separate finish launch instead
+  b->chainable = P0.paired && cmve::eval_batch_chainable(P0.sq, P0.sg, P0.c);
   hipError_t e = hipMalloc(&b->d_items, sizeof(cmve::EvalItem) * (size_t)count);
   if (e == hipSuccess) e = hipMalloc(&b->d_args, sizeof(SimArgs) * (size_t)count);
   if (e == hipSuccess)
@@ -2493,11 +2461,10 @@ extern "C" int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve
 }
 
 // timing_slot >= 0: the three launches' own start / stop into that slot of h's ring (cmve_eval_kernel_timing:
-// prep, rank GEMM, 0, finish -- durations of the whole batch's launches) and the event spans (cmve_eval_timing)
-// ps: the prep launch's stream (h->stream, or cmve_eval_batch_run_split's prep stream: it first waits for the work
-// enqueued on h->stream, and the rank GEMM waits for the prep)
-static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, int32_t timing_slot,
-                          bool chained = false, cmve_eval_batch_t prev = nullptr) {
+// prep, rank GEMM, 0, finish -- durations of the whole batch's launches) and the event spans (cmve_eval_timing).
+// A chained run's prep slot includes the previous batch's finish (fused into the prep launch, or its own launch)
+static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_slot, bool chained = false,
+                          cmve_eval_batch_t prev = nullptr) {
   hipEvent_t* ev = nullptr;
   hipEvent_t* kev = nullptr;
   if (timing_slot >= 0) {
@@ -2514,32 +2481,22 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, hipStream_t ps, 
     if (kev) cmve::g_launch_ev = cmve::LaunchEv{kev[2 * k], kev[2 * k + 1]};
   };
   hipStream_t s = h->stream;
-  const bool split = ps != s;
-  if (split) {
-    if (!b->ev_in) CMVE_HIP(hipEventCreateWithFlags(&b->ev_in, hipEventDisableTiming));
-    if (!b->ev_prep) CMVE_HIP(hipEventCreateWithFlags(&b->ev_prep, hipEventDisableTiming));
-    CMVE_HIP(hipEventRecord(b->ev_in, s));  // (the batch's previous run and whatever the caller enqueued before)
-    CMVE_HIP(hipStreamWaitEvent(ps, b->ev_in, 0));
-  }
   int st = CMVE_OK;
   const bool fused = chained && b->chainable;  // the prep and the previous batch's finish in one launch
-  if (chained && prev && !fused) {  // (not the specialised prep: the previous batch's finish as a launch of its own)
-    st = cmve::launch_eval_batch(prev->sq0, prev->sg0, prev->c0, prev->d_items, prev->count, prev->qf, prev->gf, 2, ps);
+  if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
+  if (chained && prev && !fused) {  // (not the specialised prep: the previous batch's finish as a launch of its own,
+    // inside the prep's timing span; its own kernel events are not taken -- slot 0's kernel pair times the prep)
+    st = cmve::launch_eval_batch(prev->sq0, prev->sg0, prev->c0, prev->d_items, prev->count, prev->qf, prev->gf, 2, s);
     if (st) return st;
   }
-  if (ev) CMVE_HIP(hipEventRecord(ev[0], ps));
   arm(0);
   if (fused)
     st = cmve::launch_eval_batch_chained(b->sq0, b->sg0, b->c0, b->d_items, prev ? prev->d_items : nullptr, b->count,
-                                         b->qf, b->gf, ps);
+                                         b->qf, b->gf, s);
   else
-    st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, ps);
+    st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, b->paired ? 3 : 0, s);
   if (st) return st;
-  if (ev) CMVE_HIP(hipEventRecord(ev[1], ps));
-  if (split) {
-    CMVE_HIP(hipEventRecord(b->ev_prep, ps));
-    CMVE_HIP(hipStreamWaitEvent(s, b->ev_prep, 0));
-  }
+  if (ev) CMVE_HIP(hipEventRecord(ev[1], s));
   arm(1);
   switch (b->mode) {
     case CMVE_SIM_F16: st = launch_rank_batch<CMVE_SIM_F16>(b->d_args, b->count, b->nq_pad, b->ng_pad, b->bm, b->bn, s); break;
@@ -2567,7 +2524,7 @@ extern "C" int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t
   CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS, "cmve_eval_batch_run: bad timing slot");
   CMVE_REQUIRE(!b->pending, "cmve_eval_batch_run: the batch's last chained run is not finished (chain it as the previous "
                             "batch of the next chained run, or call cmve_eval_batch_finish)");
-  return eval_batch_run(h, b, h->stream, timing_slot);
+  return eval_batch_run(h, b, timing_slot);
 }
 
 extern "C" int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t b, cmve_eval_batch_t prev,
@@ -2588,8 +2545,15 @@ extern "C" int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t b,
       CMVE_REQUIRE(std::find(prev->ws.begin(), prev->ws.end(), w) == prev->ws.end(),
                    "cmve_eval_batch_run_chained: the batch shares a workspace with the previous batch, whose finish "
                    "runs in the same launch as its prep");
+    // the prep zeroes out[0, 13) while the previous finish adds its R@K counts / rank sums into its own out
+    const uintptr_t span = sizeof(int64_t) * (uintptr_t)(CMVE_EVAL_OUT_HEAD + b->sq0.n + b->sg0.n);
+    for (void* o : b->outs)
+      for (void* po : prev->outs)
+        CMVE_REQUIRE((uintptr_t)o + span <= (uintptr_t)po || (uintptr_t)po + span <= (uintptr_t)o,
+                     "cmve_eval_batch_run_chained: the batch shares an output with the previous batch, whose finish "
+                     "runs in the same launch as its prep");
   }
-  const int st = eval_batch_run(h, b, h->stream, timing_slot, true, prev);
+  const int st = eval_batch_run(h, b, timing_slot, true, prev);
   if (st) return st;
   if (prev) prev->pending = false;
   b->pending = true;
@@ -2607,33 +2571,8 @@ extern "C" int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t b) {
   return CMVE_OK;
 }
 
-extern "C" int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t b, void* prep_stream, int32_t timing_slot) {
-  CMVE_REQUIRE(h && b && b->d_items && b->d_args && prep_stream, "cmve_eval_batch_run_split: NULL argument");
-  CMVE_REQUIRE(timing_slot >= -1 && timing_slot < CMVE_EVAL_TIMING_SLOTS,
-               "cmve_eval_batch_run_split: bad timing slot");
-  CMVE_REQUIRE(!b->pending, "cmve_eval_batch_run_split: the batch's last chained run is not finished");
-  return eval_batch_run(h, b, (hipStream_t)prep_stream, timing_slot);
-}
-
-// a stream whose kernels run only on the CUs set in mask (bit i of word i / 32: CU i), hipExtStreamCreateWithCUMask
-extern "C" int cmve_stream_create_cu_mask(const uint32_t* mask, int32_t nwords, void** stream) {
-  CMVE_REQUIRE(mask && nwords > 0 && stream, "cmve_stream_create_cu_mask: NULL argument");
-  hipStream_t st = nullptr;
-  CMVE_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)nwords, mask));
-  *stream = (void*)st;
-  return CMVE_OK;
-}
-
-extern "C" int cmve_stream_destroy(void* stream) {
-  CMVE_REQUIRE(stream, "cmve_stream_destroy: NULL stream");
-  CMVE_HIP(hipStreamDestroy((hipStream_t)stream));
-  return CMVE_OK;
-}
-
 extern "C" int cmve_eval_batch_destroy(cmve_eval_batch_t b) {
   if (!b) return CMVE_OK;
-  if (b->ev_in) (void)hipEventDestroy(b->ev_in);
-  if (b->ev_prep) (void)hipEventDestroy(b->ev_prep);
   (void)hipFree(b->d_items);
   (void)hipFree(b->d_args);
   delete b;

@@ -709,10 +709,12 @@ extern "C" int cmve_topk(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_
   rc = check_launch("topk_collect_kernel");
   if (rc) return rc;
 
-  // 5. select + exact re-score + sort.  CMVE_TOPK_DENSE=1 (tests only) sends every query down the
-  // dense-row path that a candidate-list overflow takes.
-  const char* dense_env = getenv("CMVE_TOPK_DENSE");
-  const int64_t list_cap = (dense_env && atoi(dense_env)) ? -1 : CAND_CAP;
+  // 5. select + exact re-score + sort.  A study build with -DCMVE_TOPK_DENSE=1 sends every query down the
+  // dense-row path that a candidate-list overflow takes (tests reach it through near-duplicate galleries).
+#ifndef CMVE_TOPK_DENSE
+#define CMVE_TOPK_DENSE 0
+#endif
+  const int64_t list_cap = CMVE_TOPK_DENSE ? -1 : CAND_CAP;
 #define TK(TQ, TG)                                                                                                 \
   hipLaunchKernelGGL((topk_finish_kernel<TQ, TG>), dim3((unsigned)q->n), dim3(TOPK_THREADS), 0, st, scores,       \
                      g->n_pad, g->n, k, cnt, cand, (const TQ*)q->raw, q->raw_ld, q->inv_norm, qerr,                \

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CMVE_ABI_VERSION 20
+#define CMVE_ABI_VERSION 21
 
 enum cmve_status {
   CMVE_OK = 0,
@@ -325,20 +325,6 @@ int cmve_rank_mfma(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, 
 int cmve_rank_fixup(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
                     const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
                     const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count);
-/* The same re-score with the undecided pairs first regrouped: `group` consecutive gallery buckets
- * (0 = as many as keep their raw rows within 2 MiB) form a super-bucket whose pairs are counting-sorted
- * by query tile into `scratch` (caller-owned, uint64[scratch_cap], scratch_cap >=
- * cmve_rank_fixup_tiled_scratch(q, g, cand_cap, group)), so each query row is fetched once per
- * (super-bucket, query tile) instead of once per pair.  For lists with many pairs per (query tile,
- * gallery bucket) -- the MultiFusion CIRR ranking.  Counts identical to cmve_rank_fixup.
- * Replaces: the argsort of MultiFusion/src/validate.py:71-105 (with cmve_rank_mfma). */
-int cmve_rank_fixup_tiled(cmve_handle_t h, const cmve_rows_t* q, const cmve_rows_t* g, int32_t dirs,
-                          const double* row_sgt, const double* col_sgt, int32_t* row_cnt, int32_t* col_cnt,
-                          const uint64_t* cand, int64_t cand_cap, const int64_t* cand_count,
-                          uint64_t* scratch, int64_t scratch_cap, int32_t group);
-/* scratch words cmve_rank_fixup_tiled needs (-1 on a NULL argument); no device work */
-int64_t cmve_rank_fixup_tiled_scratch(const cmve_rows_t* q, const cmve_rows_t* g, int64_t cand_cap, int32_t group);
-
 /*
  * cmve_rank_count with the fix-up hidden behind the MFMA pass: the gallery `g` is cut into
  * `chunks` row ranges (multiples of CMVE_ROW_ALIGN); chunk c's MFMA pass runs on the handle's
@@ -459,26 +445,21 @@ int cmve_eval_batch_create(int32_t count, cmve_rows_t* const* q, cmve_rows_t* co
 /* timing_slot: -1, or a slot of h's timing ring receiving the batch's launch durations (cmve_eval_kernel_timing:
  * prep, rank GEMM, 0, finish; cmve_eval_timing: the event spans), as for cmve_eval_ranks */
 int cmve_eval_batch_run(cmve_handle_t h, cmve_eval_batch_t batch, int32_t timing_slot);
-/* the same run with its prep launch on prep_stream (a hipStream_t): the prep first waits for the work enqueued on
- * h's stream, the rank GEMM and the finish (on h's stream) wait for the prep.  With the prep stream and the batch
- * streams on disjoint CU sets (cmve_stream_create_cu_mask) one batch's HBM-bound prep runs beside another's rank
- * GEMM instead of taking every CU in turn.  Results are those of cmve_eval_batch_run. */
-int cmve_eval_batch_run_split(cmve_handle_t h, cmve_eval_batch_t batch, void* prep_stream, int32_t timing_slot);
 /* Chained runs of a stream's successive batches (the headline's validation loop: LINAS-engine/validate.py:61-74 once
  * per evaluation): the run of `batch` defers its finish (ranks, R@K, pair total: the outputs' words) to the next
  * chained run on h's stream, whose first launch holds that finish beside its own prep (the specialised paired prep:
  * one launch; otherwise the finish runs as a launch of its own first).  prev: the batch chained on this stream
  * before (NULL: none); its outputs are complete once this call's first launch has run.  cmve_eval_batch_finish runs
  * a batch's deferred finish alone (after a stream's last chained run).  prev must have the batch's shapes and share
- * no workspace with it.  Results equal cmve_eval_batch_run's bit for bit; timing_slot records the launches
- * (cmve_eval_kernel_timing: prep (with the previous finish), rank GEMM, fix-up, 0).  A batch whose chained run
+ * no workspace and no output range with it (refused otherwise: its finish adds into its outputs while this batch's
+ * prep zeroes them).  Results equal cmve_eval_batch_run's bit for bit; timing_slot records the launches
+ * (cmve_eval_timing: the prep span includes the previous finish; cmve_eval_kernel_timing: prep (the fused launch
+ * with the previous finish, or the prep launch alone when the finish ran as a launch of its own), rank GEMM,
+ * fix-up, 0).  A batch whose chained run
  * awaits its finish is refused by every run call until that finish is enqueued (as the prev of the next chained
  * run on the same stream, or by cmve_eval_batch_finish on it); prev must be such a batch of h's stream. */
 int cmve_eval_batch_run_chained(cmve_handle_t h, cmve_eval_batch_t batch, cmve_eval_batch_t prev, int32_t timing_slot);
 int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t batch);
-/* a HIP stream restricted to the CUs set in mask (bit i of word i / 32 = CU i; hipExtStreamCreateWithCUMask) */
-int cmve_stream_create_cu_mask(const uint32_t* mask, int32_t nwords, void** stream);
-int cmve_stream_destroy(void* stream);
 int cmve_eval_batch_destroy(cmve_eval_batch_t batch);
 typedef struct cmve_eval_graph* cmve_eval_graph_t;
 int cmve_eval_graph_create(cmve_handle_t h, cmve_rows_t* q, cmve_rows_t* g, int32_t mode,

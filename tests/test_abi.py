@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     from cmve import _lib
-    assert _lib.lib.cmve_abi_version() == 20
+    assert _lib.lib.cmve_abi_version() == 21
     n_pad, d_pad = C.c_int64(), C.c_int64()
     assert _lib.lib.cmve_pack_size(1000, 1024, C.byref(n_pad), C.byref(d_pad)) == 0
     assert (n_pad.value, d_pad.value) == (1024, 1024)
@@ -81,22 +81,3 @@ def test_eval_workspace_layout_host_only():
     assert b2.value - b1.value == 8 << 16
     assert b1.value >= (8 << 16) + 2 * 1024 * (8 + 4 + 4 + 4)
     assert _lib.lib.cmve_eval_workspace(C.byref(q), C.byref(g), 0, C.byref(b1)) < 0
-
-
-def test_tiled_fixup_scratch_size():
-    """cmve_rank_fixup_tiled_scratch (host-only): the sorted copy fits the candidate buffer's capacity, plus one int32
-    bin count per (super-bucket, query tile); -1 on a NULL set."""
-    from cmve import _lib
-    q, g = _lib.Rows(), _lib.Rows()
-    q.n, q.n_pad, q.d, q.d_pad, q.raw_dtype = 30364, 30464, 640, 640, _lib.CMVE_F32
-    g.n, g.n_pad, g.d, g.d_pad, g.raw_dtype = 44493, 44544, 640, 640, _lib.CMVE_F32
-    cap = 1 << 24
-    nb = g.n_pad // 256
-    nbins = (q.n_pad - 1) // 256 + 1
-    f = _lib.lib.cmve_rank_fixup_tiled_scratch
-    for group in (1, 2, 3, 5, 64):
-        nsb = -(-nb // group)
-        assert f(C.byref(q), C.byref(g), cap, group) == cap + (nsb * nbins + 1) // 2
-    # group 0: super-buckets of raw gallery rows within 2 MiB (256 x 640 fp32 = 640 KiB per bucket -> 3)
-    assert f(C.byref(q), C.byref(g), cap, 0) == f(C.byref(q), C.byref(g), cap, 3)
-    assert f(None, C.byref(g), cap, 0) == -1

@@ -190,3 +190,74 @@ def test_rank_batch_chained_general_prep(torch_cuda):
         for s, r in zip(sess, rs):
             assert torch.equal(s.out, r)
         rb.close()
+
+
+@pytest.mark.parametrize("nq,ng", [(700, 900), (900, 600)])
+def test_rank_batch_chained_f16_multi_gt(torch_cuda, nq, ng):
+    """An F16 batch whose lists are no one-to-one pairing (multi-GT captions, n_q != n_g) at d = 512 takes the
+    general prep in run(); its chained runs must not fuse the specialised PAIRED prep with the previous finish
+    (which packs only the GT partners' gallery rows, and writes gallery rows at caption indices): every output word
+    equals run()'s, and the ranks equal the oracle's exact counts."""
+    torch = torch_cuda
+    from cmve import engine
+    rng = np.random.default_rng(31)
+    d = 512
+    rows = [[int(x) for x in rng.choice(ng, size=1 + i % 3, replace=False)] for i in range(nq)]
+    cols = [[] for _ in range(ng)]
+    for i, l in enumerate(rows):
+        for j in l:
+            cols[j].append(i)
+    bats, ref, host = [], [], []
+    for b in range(3):
+        sets, sess = [], []
+        for j in range(2):
+            gal = rng.standard_normal((ng, d))
+            qs = gal[[l[0] for l in rows]] + 0.9 * rng.standard_normal((nq, d))
+            host.append((qs, gal))
+            sets.append((torch.from_numpy(qs).cuda(), torch.from_numpy(gal).cuda()))
+            sess.append(engine.RankSession(nq, ng, d, row_gts=rows, col_gts=cols, dtype=torch.float64))
+        assert not sess[0].paired
+        rb = engine.RankBatch(sess, sets)
+        rb.run()
+        torch.cuda.synchronize()
+        ref.append([s.out.clone() for s in sess])
+        for s in sess:
+            s.out[:13].fill_(-7)
+            s.out[16:].fill_(-7)
+        bats.append((rb, sess))
+    prev = None
+    for bi in [0, 1, 2, 0]:
+        bats[bi][0].run_chained(prev)
+        prev = bats[bi][0]
+    prev.finish()
+    torch.cuda.synchronize()
+    for (rb, sess), rs in zip(bats, ref):
+        for s, r in zip(sess, rs):
+            assert torch.equal(s.out, r), (s.out[:16].tolist(), r[:16].tolist())
+    qs, gal = host[0]
+    s = R.exact_scores64(qs, gal)
+    h = bats[0][1][0].out.cpu().numpy()
+    assert np.array_equal(h[16:16 + nq], R.rank_counts(s, rows)) and np.array_equal(h[16 + nq:], R.rank_counts(s.T, cols))
+    for rb, _ in bats:
+        rb.close()
+
+
+def test_rank_batch_chained_refuses_shared_outputs(torch_cuda):
+    """Two batches writing one output block: a chained run of one after the other is refused (the second's prep zeroes
+    the R@K head the first's finish adds into, in the same launch); run() of either stays allowed."""
+    torch = torch_cuda
+    from cmve import engine
+    groups, n_q = _groups(torch, 2, 2)
+    n_out = groups[0][0][0].out.numel()
+    shared = torch.zeros((2, n_out), dtype=torch.int64, device="cuda")
+    b0 = engine.RankBatch(groups[0][0], groups[0][1], outs=list(shared))
+    b1 = engine.RankBatch(groups[1][0], groups[1][1], outs=list(shared))
+    b0.run()
+    b1.run()
+    b0.run_chained(None)
+    with pytest.raises(RuntimeError, match="shares an output"):
+        b1.run_chained(b0)
+    b0.finish()
+    torch.cuda.synchronize()
+    b0.close()
+    b1.close()

@@ -4,7 +4,6 @@ Bars: integer ranks / top-k ids bit-exact; cosine scores within 1e-4 (north star
 split-bf16 store path is checked at 1e-5); every bf16 MFMA score within its stated
 rigorous error bound.
 """
-import os
 
 import numpy as np
 import pytest
@@ -396,18 +395,10 @@ def test_rank_session_replays_match(golden, torch_cuda, dtype):
                                         row_gts=rows, col_gts=v2t_gt)
     assert np.array_equal(t2v2, e_t) and np.array_equal(v2t2, e_v)
     # at this size (G64) the rank GEMM re-scores its undecided pairs itself: no list, so a tiny one cannot
-    # overflow; with the separate fix-up launch (CMVE_EVAL_FIX_LAUNCH=1) the same ranks, and a tiny list
-    # overflows, grows and redoes the evaluation
+    # overflow
     sess._alloc(600)
     t2v3, v2t3 = sess.run(ct, vt)
     assert sess.cap == 600 and np.array_equal(t2v3, t2v) and np.array_equal(v2t3, v2t)
-    os.environ["CMVE_EVAL_FIX_LAUNCH"] = "1"
-    try:
-        t2v4, v2t4 = sess.run(ct, vt)
-        assert sess.cap > 600 and sess.ncand == ncand - len(cid)
-        assert np.array_equal(t2v4, t2v) and np.array_equal(v2t4, v2t)
-    finally:
-        del os.environ["CMVE_EVAL_FIX_LAUNCH"]
 
 
 def _nan_case(g, tag):
@@ -870,63 +861,6 @@ def test_level2_rescore_near_ties(torch_cuda, noise, seed):
 
 
 @pytest.mark.gpu
-def test_rank_batch_run_split_streams(golden, torch_cuda):
-    """cmve_eval_batch_run_split: the batch's prep on a stream of its own over half the CUs
-    (cmve_stream_create_cu_mask), the rank GEMM + finish on the batch's stream over the other half: every output
-    word equals the plain run's, run after run (the prep waits for the batch's previous finish)."""
-    import torch
-    from cmve import engine
-    v, c, vid, cid = _c1()
-    v2t_gt, t2v_gt = R.get_gt(vid, cid)
-    rows, cols = [t2v_gt[i] for i in range(len(cid))], v2t_gt
-    n_q, n_g, d = c.shape[0], v.shape[0], c.shape[1]
-    rng = np.random.default_rng(11)
-    sets = [(torch.from_numpy(c if j == 0 else c + 0.3 * rng.standard_normal(c.shape)).cuda(),
-             torch.from_numpy(v).cuda()) for j in range(3)]
-    ref_s = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64) for _ in sets]
-    ref_b = engine.RankBatch(ref_s, sets)
-    ref_b.run()
-    torch.cuda.synchronize()
-    ref = [x.out.clone() for x in ref_s]
-    ref_b.close()
-    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
-    ps = engine.cu_mask_stream("cuda:0", [k for k in range(n_cu) if k % 2 == 0])
-    gs = engine.cu_mask_stream("cuda:0", [k for k in range(n_cu) if k % 2 == 1])
-    sess = [engine.RankSession(n_q, n_g, d, row_gts=rows, col_gts=cols, dtype=torch.float64, stream=gs) for _ in sets]
-    b = engine.RankBatch(sess, sets, stream=gs)
-    for _ in range(3):
-        b.run(prep_stream=ps)
-    torch.cuda.synchronize()
-    for x, r in zip(sess, ref):
-        assert torch.equal(x.out, r)
-    g = golden("retrieval_c1")
-    h = sess[0].out.cpu().numpy()
-    assert np.array_equal(h[16:16 + n_q], g["t2v_ranks"]) and np.array_equal(h[16 + n_q:], g["v2t_ranks"])
-    b.close()
-    # (the streams stay open: the inputs read in place were recorded on gs, and the caching allocator records an
-    # event on it when they are freed -- test_cu_mask_stream_close closes a stream nothing was recorded on)
-
-
-@pytest.mark.gpu
-def test_cu_mask_stream_close(torch_cuda):
-    """cu_mask_stream refuses an empty CU list; close_cu_mask_stream destroys the stream once (a second close is an
-    error); work launched on it before the close completes."""
-    torch = torch_cuda
-    from cmve import engine
-    with pytest.raises(ValueError, match="no CU"):
-        engine.cu_mask_stream("cuda:0", [])
-    st = engine.cu_mask_stream("cuda:0", [0, 1, 2, 3])
-    x = torch.arange(1 << 20, device="cuda:0", dtype=torch.float32)
-    torch.cuda.synchronize()
-    with torch.cuda.stream(st):
-        y = x * 2.0
-    engine.close_cu_mask_stream(st)
-    assert float(y[-1]) == 2.0 * ((1 << 20) - 1)
-    with pytest.raises(ValueError, match="not a live"):
-        engine.close_cu_mask_stream(st)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("d", [512, 768])
 def test_paired_prep_plane_widths(torch_cuda, d):
     """The paired fp16 prep writes its fp16 and bf16-residual planes write-through in 16-B pieces, lanes L and L ^ 1
@@ -1022,7 +956,6 @@ def test_level3_list_overflow(torch_cuda, batched):
         sess = engine.RankSession(n, n, d, row_gts=ids, col_gts=ids, dtype=torch.float64)
         sess.run(ct, vt)
         outs = [sess.out.cpu().numpy()]
-    inline_l2 = os.environ.get("CMVE_EVAL_INLINE_L2", "") != "0"  # (the default; the fix-up launch form,
-    for h in outs:  # CMVE_EVAL_INLINE_L2=0, keeps no level-3 list: out[12] = 0)
-        assert h[9] == 0 and (h[12] > 4096 if inline_l2 else h[12] == 0), (h[8], h[12])
+    for h in outs:
+        assert h[9] == 0 and h[12] > 4096, (h[8], h[12])
         assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)

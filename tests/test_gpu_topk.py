@@ -85,23 +85,6 @@ def test_topk_nan_rows_and_k_beyond_finite(torch_cuda):
         _check(idx, sc, s, k)
 
 
-def test_topk_dense_fallback_matches(torch_cuda, monkeypatch):
-    """The dense-row path (taken when a query's candidate list overflows) gives the same result."""
-    from cmve import engine
-    rng = np.random.default_rng(9)
-    gal = rng.standard_normal((50000, 256)).astype(np.float32)
-    qs = (gal[rng.integers(0, 50000, 5)] + 2.0 * rng.standard_normal((5, 256))).astype(np.float32)
-    s = R.exact_scores64(qs, gal)
-    q = engine.RowSet(qs, with_lo=True)
-    g = engine.RowSet(gal, with_lo=True)
-    a = engine.topk(q, g, 20)
-    monkeypatch.setenv("CMVE_TOPK_DENSE", "1")
-    b = engine.topk(q, g, 20)
-    monkeypatch.delenv("CMVE_TOPK_DENSE")
-    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
-    _check(b[0], b[1], s, 20)
-
-
 def test_topk_near_duplicates(torch_cuda):
     """A dense cluster of near-duplicate videos around the best match: many candidates share the
     histogram bins of the k-th score; ids stay exact."""

@@ -72,7 +72,9 @@ def main(outdir, tag):
         out["trace_launches"] = len(ms)
         out["trace_avg_ms_all"] = sum(ms) / len(ms)
         out["trace_avg_ms_timed"] = sum(ms[-steps:]) / len(ms[-steps:])
-    out.update({"shard": 131072, "nq": 16384, "dim": 1024, "chunks": 1,
+    # the leg profiled: gallery_shard (defaults) or gallery_1m (SHARD=1048576 CHUNKS=8: each launch one chunk)
+    out.update({"shard": int(os.environ.get("SHARD", "131072")), "nq": 16384, "dim": 1024,
+                "chunks": int(os.environ.get("CHUNKS", "1")),
                 "correction": "2 x FETCH_SIZE (gfx950 half-count on wide reads) + WRITE_SIZE, KiB -> bytes"})
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
     print(json.dumps(out))
