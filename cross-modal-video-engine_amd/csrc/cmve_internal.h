@@ -495,19 +495,6 @@ __device__ __forceinline__ double l16_partial(const L16Frag& a, const L16Frag& b
     acc = fma(l16_x(ah[e >> 1], al[e >> 1], e & 1), l16_x(bh[e >> 1], bl[e >> 1], e & 1), acc);
   return acc;
 }
-// one pair's level-2 score (every lane gets the same bits): rows of the fp16 and bf16 residual planes, d_pad % 64 == 0
-__device__ __forceinline__ double l16_score1(const uint16_t* hq, const uint16_t* lq, const uint16_t* hg,
-                                             const uint16_t* lg, int64_t d_pad, int lane) {
-  double acc = 0.0;
-  for (int64_t k = 16 * (int64_t)lane; k < d_pad; k += 1024) {
-    L16Frag a, b;
-    l16_load(hq, lq, k, a);
-    l16_load(hg, lg, k, b);
-    acc = l16_partial(a, b, acc);
-  }
-  return wave_sum(acc);
-}
-
 // XCD-ordered re-score of the bucketed undecided pairs: XCD x (blockIdx & 7) owns buckets
 // x, x+8, ...; its waves stride through those buckets' pairs in order, so at any time an XCD works
 // on one or two buckets and their raw gallery rows (1 MiB each) stay in its L2.
@@ -515,18 +502,6 @@ __device__ __forceinline__ double l16_score1(const uint16_t* hq, const uint16_t*
 // bandwidth-bound bench-size fix-up that was 3% slower)
 // flat: one group over all buckets and every wave of the grid (small evaluations: a 1k-row gallery has
 // 4 buckets, which the XCD grouping would leave to 4 of the 8 XCDs); the caller keeps nb <= 4096
-// the level-2 planes of an evaluation's fix-up (K14 with the bf16 residual planes): h16 / lo16 of both sets, their
-// per-row bounds and the plane stride; qh == nullptr: every pair in fp64
-struct L2Planes {
-  const uint16_t* qh = nullptr;
-  const uint16_t* ql = nullptr;
-  const uint16_t* gh = nullptr;
-  const uint16_t* gl = nullptr;
-  const float* qe = nullptr;
-  const float* ge = nullptr;
-  int64_t ldk = 0;
-};
-
 // the exclusive prefix of the bucket sizes a fix-up walks (wave 0 of the block): buckets xcd, xcd + G, ..., nk
 // of them, each clamped to cap_b; pre[nk] = the total (lane-chunked sums + a wave scan)
 __device__ __forceinline__ void fixup_prefix(const uint64_t* __restrict__ cand, int64_t nb, int64_t cap_b, int xcd,
@@ -577,8 +552,7 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
                                                     const double* __restrict__ row_sgt,
                                                     const double* __restrict__ col_sgt, int* __restrict__ row_cnt,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
-                                                    int64_t nb, int64_t cap_b, bool flat = false,
-                                                    const L2Planes l2 = L2Planes{}) {
+                                                    int64_t nb, int64_t cap_b, bool flat = false) {
   int64_t* pre;
   if constexpr (DYN_PRE) {
     extern __shared__ int64_t fix_dyn_pre[];
@@ -621,29 +595,7 @@ __device__ __forceinline__ void fixup_walk(const TQ* __restrict__ qraw, int64_t 
     const int64_t i = (int64_t)(u & 0x7fffffffull);
     const int64_t j = (int64_t)((u >> 31) & 0x7fffffffull);
     uint32_t flags = (uint32_t)(u >> 62);
-    if (l2.qh && flags) {
-      // level 2: the pair from the fp16 + bf16 residual planes (one round trip of 8 KiB, the planes the rank GEMM
-      // just read); a direction whose GT score lies outside s2 +- E2 is decided here, the rest in fp64 below
-      const double s2 = l16_score1(l2.qh + i * l2.ldk, l2.ql + i * l2.ldk, l2.gh + j * l2.ldk, l2.gl + j * l2.ldk,
-                                   l2.ldk, lane);
-      const double eq = (double)gld(l2.qe + i), eg = (double)gld(l2.ge + j);
-      const double E2 = eq + (1.0 + eq) * eg + 2e-12;
-      if ((flags & 1u) && row_sgt) {
-        const double t = gld(row_sgt + i);
-        if (s2 - E2 > t || s2 + E2 < t) {
-          if (s2 - E2 > t && lane == 0) gadd(row_cnt + i, 1);
-          flags &= ~1u;
-        }
-      }
-      if ((flags & 2u) && col_sgt) {
-        const double t = gld(col_sgt + j);
-        if (s2 - E2 > t || s2 + E2 < t) {
-          if (s2 - E2 > t && lane == 0) gadd(col_cnt + j, 1);
-          flags &= ~2u;
-        }
-      }
-    }
-    if (!flags) continue;  // (decided at level 2, or a null entry)
+    if (!flags) continue;  // (a null entry)
     double rs = 0.0, cs = 0.0;
     if (PREFETCH) {
       rs = ((flags & 1u) && row_sgt) ? gld(row_sgt + i) : 0.0;

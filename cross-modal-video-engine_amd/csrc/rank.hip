@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(const TQ* __restrict__ qraw,
                                                     int* __restrict__ col_cnt, const uint64_t* __restrict__ cand,
                                                     int64_t nb, int64_t cap_b) {
   fixup_walk<TQ, TG, PF, true, true>(qraw, ldq, qinv, graw, ldg, ginv, d, row_sgt, col_sgt, row_cnt, col_cnt, cand, nb,
-                                     cap_b, false, L2Planes{});
+                                     cap_b, false);
 }
 
 // the walk over nb buckets of cap_b entries at cand (counts at cand[0, nb)).  Every wave has one pair in flight.

@@ -4,7 +4,8 @@ scaling): 16,384 captions x 1,048,576 videos x 1024-d, exact t2v GT ranks throug
 
 Properties at full size (no CPU oracle can score 1.7e10 pairs in a test): every rank in [1, n_g], the recall sums
 monotone, the same gallery / captions regardless of the rank count (strong_gallery_inputs), and 256 sampled captions
-equal to independent fp64 torch GEMMs over the whole gallery (bit-exact ranks)."""
+equal to independent fp64 torch GEMMs over the whole gallery (bit-exact ranks), 16 of them also to the CPU oracle itself
+(oracle/retrieval.py exact_scores64 + rank_counts over all 1,048,576 gallery rows)."""
 import numpy as np
 import pytest
 
@@ -36,3 +37,9 @@ def test_gallery_1m_single_gpu_ranks_against_fp64():
     print(f"1M gallery: R@1 {100 * r1 / nq:.2f} R@10 {100 * r10 / nq:.2f}, "
           f"{int((got != exp).sum())} of {got.size} sampled ranks differ from fp64")
     assert np.array_equal(got, exp)
+    # the oracle on 16 of the sampled captions (fp64 l2norm + GEMM + rank count on the host, ~2 s)
+    from oracle import retrieval as R
+    sub = sample[::16]
+    s64 = R.exact_scores64(q[sub.to(dev)].cpu().numpy(), gallery.cpu().numpy())
+    exp_o = R.rank_counts(s64, [gts[i] for i in sub.tolist()])
+    assert np.array_equal(ranks[sub.numpy()], exp_o)

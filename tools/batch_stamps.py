@@ -1,5 +1,5 @@
 """Kernel study of a K14 batch (cmve_eval_batch_*): s_memrealtime stamps (100 MHz) of every rank tile of the
-batch's evaluations (CMVE_EVAL_DBG=128, a diagnostic mode: timings only) plus the first evaluation's prep and
+batch's evaluations (a diagnostic build: make study NAME=stamps DEFS=-DCMVE_EVAL_DBG=128, loaded with CMVE_LIB=.../libcmve_stamps.so; timings only) plus the first evaluation's prep and
 finish blocks.  Prints medians over 20 batch runs: the launch spans, the per-tile phase durations and the
 tile duration percentiles, in microseconds from the first prep block's start."""
 import ctypes
@@ -7,7 +7,6 @@ import json
 import os
 import sys
 
-os.environ["CMVE_EVAL_DBG"] = "128"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "cross-modal-video-engine_amd"), ROOT, os.path.join(ROOT, "tests", "golden")):
     sys.path.insert(0, p)

@@ -1,5 +1,5 @@
 """Kernel study of the K14 evaluation: s_memrealtime stamps (100 MHz) per block of the prep, fix-up and
-finish launches (CMVE_EVAL_DBG=128, a diagnostic mode: timings only; the rank GEMM carries none).
+finish launches (a diagnostic build: make study NAME=stamps DEFS=-DCMVE_EVAL_DBG=128, loaded with CMVE_LIB; timings only; the rank GEMM carries none).
 Prints, per launch, the first / last block start and the first / last block end, in microseconds from
 the first prep block's start, median over 30 evaluations."""
 import ctypes
@@ -7,7 +7,6 @@ import json
 import os
 import sys
 
-os.environ["CMVE_EVAL_DBG"] = str(128 | int(os.environ.get("STAMPS_DBG", "0")))  # + study bits (results garbage)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "cross-modal-video-engine_amd"), ROOT, os.path.join(ROOT, "tests", "golden")):
     sys.path.insert(0, p)
