@@ -48,6 +48,9 @@
 #ifndef CMVE_EVAL_L3_LIST
 #define CMVE_EVAL_L3_LIST 0  // 1: one evaluation lists its level-3 pairs for the finish as batches do
 #endif
+#ifndef CMVE_G64_KG
+#define CMVE_G64_KG 2  // one K14 evaluation's G64 rank GEMM: K groups (2: split-K over two groups of 4 waves)
+#endif
 
 namespace cmve {
 
@@ -432,9 +435,15 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_BATCH_WPE
 #define CMVE_BATCH_WPE 4  // the batch ring kernels: waves per SIMD the register budget must allow (<= 128 VGPRs)
 #endif
-template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false>
-__global__ __launch_bounds__(WM * WN * 64, BATCH ? ((is_big_ring<WM * TM * 16, WN * 64>() || WM * WN == 4) ? 2 : CMVE_BATCH_WPE)
-                                                 : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2))
+// KG = 2 (one K14 evaluation's G64 rank GEMM, sim_kernel_kg2): two groups of WM x WN waves, each streaming half of
+// the K-tiles through a ring of its own; the second group's partial sums are added to the first's through LDS
+// before the epilogue (every output element: two fp32 MFMA chains of d/2 then one fp32 add -- inside the same error
+// bound, fewer roundings than one chain), and both groups share the level-2 re-score
+template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false, int KG = 1>
+__global__ __launch_bounds__(WM * WN * 64 * KG,
+                            KG > 1 ? 1
+                                   : (BATCH ? ((is_big_ring<WM * TM * 16, WN * 64>() || WM * WN == 4) ? 2 : CMVE_BATCH_WPE)
+                                            : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2)))
 void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
   // a batch's blocks: the (evaluation, tile) pairs in evaluation-major order, cut into 8 contiguous ranges, one per
@@ -458,7 +467,10 @@ void sim_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar M0 / soffset
-  const int wr = wave / WN, wc = wave % WN;
+  // KG = 2: group = which half of K this wave streams, lw = its wave within the group (the output layout)
+  constexpr int NWT = NW * KG, NTT = NT * KG;
+  const int group = KG > 1 ? wave / NW : 0, lw = wave - group * NW;
+  const int wr = lw / WN, wc = lw % WN;
   // tiles: the phased (G256) kernel is persistent -- one block per CU walks tile, tile + gridDim.x,
   // ... (same XCD, same XCD-local order as a one-tile-per-block grid); the G128 grid is one tile each
   const int ntiles = a.nblk_m * a.nblk_n;
@@ -549,7 +561,7 @@ void sim_kernel(
   if constexpr (EPI_COLS) fetch_cols(n0, colv);
   if constexpr (epi_thr(EPI)) {
     static_assert(NT >= BM + BN, "one threshold pair per thread (threads past BM + BN hold none)");
-    for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;  // later tiles: reset by the flush
+    for (int t = tid; t < BM + BN; t += NTT) lds_rc[t] = 0;  // later tiles: reset by the flush
     // K14 thresholds need the block's err_max reduction first: the 2-stage / ring loops do both after
     // issuing their first loads (below).  The persistent G256 kernel never derives them (cmve_eval_ranks
     // writes them with eval_thr_kernel first): the derivation's code alone cost it 18% (SGPR spills at
@@ -561,13 +573,13 @@ void sim_kernel(
 #ifdef CMVE_DBG_NOLOAD
     return;
 #endif
-    char* base = smem + s * STAGE_BYTES;
+    char* base = smem + (group * NS + s) * STAGE_BYTES;  // (KG = 2: each group's ring of its own)
     const int k0 = t * KB;
-    stage_plane<BM, NW, KB>(a.qhi, a.ldk, m0, k0, base, wave, lane);
-    stage_plane<BN, NW, KB>(a.ghi, a.ldk, n0, k0, base + A_BYTES, wave, lane);
+    stage_plane<BM, NW, KB>(a.qhi, a.ldk, m0, k0, base, lw, lane);
+    stage_plane<BN, NW, KB>(a.ghi, a.ldk, n0, k0, base + A_BYTES, lw, lane);
     if (MODE == CMVE_SIM_BF16X3) {
-      stage_plane<BM, NW, KB>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, wave, lane);
-      stage_plane<BN, NW, KB>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, wave, lane);
+      stage_plane<BM, NW, KB>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, lw, lane);
+      stage_plane<BN, NW, KB>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, lw, lane);
     }
   };
 
@@ -832,7 +844,10 @@ void sim_kernel(
             for (int r = 0; r < 4; ++r)
               if (!((rowok >> (i * 4 + r)) & (colok >> j) & 1u)) acc[i][j][r] = -INFINITY;
       }
-      if (do_row && do_col) {
+      if (KG > 1 && group != 0) {  // (KG = 2: the second group's sums were added to the first's; it scores nothing)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) und[i] = 0u;
+      } else if (do_row && do_col) {
         fast_block(std::true_type{}, std::true_type{});
       } else if (do_row) {
         fast_block(std::true_type{}, std::false_type{});
@@ -902,7 +917,7 @@ void sim_kernel(
           CMVE_BAR_LDS();
           int woff = 0, ntot = 0;
 #pragma unroll
-          for (int w = 0; w < NW; ++w) {
+          for (int w = 0; w < NWT; ++w) {
             const int t = epi.wtot[w];
             woff += w < wave ? t : 0;
             ntot += t;
@@ -936,7 +951,7 @@ void sim_kernel(
               // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
               // entries: no other wave touches them)
               constexpr int RP = BATCH ? ((is_big_ring<BM, BN>() || NW == 4) ? CMVE_L2_P_BIG : CMVE_L2_P) : CMVE_L2_P_ONE;
-              for (int p0 = wave * RP; p0 < ntot; p0 += NW * RP) {
+              for (int p0 = wave * RP; p0 < ntot; p0 += NWT * RP) {
                 int64_t qr[RP], gc[RP];
                 uint32_t ent[RP];
 #pragma unroll
@@ -1027,7 +1042,7 @@ void sim_kernel(
             // register count leaves room on each SIMD for a wave of the other stream's prep
             constexpr bool FIX1 = BATCH && CMVE_BATCH_FIX1;
             if constexpr (FIX1) {
-              for (int p = wave; p < ntot; p += NW) {
+              for (int p = wave; p < ntot; p += NWT) {
                 const uint32_t e = epi.list[p];
                 if (!(e >> 16)) continue;  // decided at level 2
                 const int64_t r1 = m0 + (e & 0xff), c1 = n0 + ((e >> 8) & 0xff);
@@ -1048,12 +1063,12 @@ void sim_kernel(
                 }
               }
             } else if (a.q_lo16) {  // level 3 after level 2 (a full level-3 list): one pair at a time per wave
-              for (int p = wave; p < ntot; p += NW) {
+              for (int p = wave; p < ntot; p += NWT) {
                 const uint32_t e = epi.list[p];
                 if (e >> 16) rescore2(e, 0u, false);
               }
             } else {
-              for (int p = 2 * wave; p < ntot; p += 2 * NW)
+              for (int p = 2 * wave; p < ntot; p += 2 * NWT)
                 rescore2(epi.list[p], p + 1 < ntot ? epi.list[p + 1] : 0u, p + 1 < ntot);
             }
           } else {
@@ -1093,11 +1108,11 @@ void sim_kernel(
       }
       CMVE_STAMP(6);
 #ifdef CMVE_DBG_NOFLUSH  // diagnostic build only: no global flush of candidates / counts (results garbage)
-      for (int t = tid; t < BM + BN; t += NT) lds_rc[t] = 0;
+      for (int t = tid; t < BM + BN; t += NTT) lds_rc[t] = 0;
       return;
 #endif
       CMVE_BAR_LDS();  // every wave's row / column count adds have landed in LDS
-      for (int t = tid; t < BM + BN; t += NT) {
+      for (int t = tid; t < BM + BN; t += NTT) {
         const int c = lds_rc[t];
         lds_rc[t] = 0;  // owner thread: ready for the next tile
         if (!c) continue;
@@ -1370,6 +1385,8 @@ void sim_kernel(
   constexpr bool KSPLIT = CMVE_RING_KSPLIT && BATCH && MODE != CMVE_SIM_BF16X3 && KS > 1;
   static_assert(LPS * (NS - 2) <= 63, "vmcnt immediate");
   const int nk0 = a.nk0 * (BK / KB);  // (a.nk0: 64-deep K-tiles; d_pad % 64 == 0)
+  // KG = 2: this wave's group streams K-tiles [kt0, kt0 + nkg) (the host launches it only for nk0 % 2 == 0)
+  const int nkg = nk0 / KG, kt0 = group * nkg;
   // K14: the other set's err_max shards as VECTOR loads, one shard per lane, issued before the first
   // K-tiles (the oldest loads: retired by the first ring wait) and folded after the main loop -- as scalar
   // loads their round trip held the prologue (~2.5 us to the first K-tile in the stamps)
@@ -1381,7 +1398,7 @@ void sim_kernel(
       emg = gld(a.g_emax + lane);
     }
   }
-  for (int t = 0; t < NS - 1 && t < nk0; ++t) stage(t, t);
+  for (int t = 0; t < NS - 1 && t < nkg; ++t) stage(kt0 + t, t);
   // K14 thresholds: the GT score / bound loads are issued behind the first K-tiles' loads and the rule
   // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
   double sgt_raw = 0.0;
@@ -1397,9 +1414,9 @@ void sim_kernel(
     }
   }
   CMVE_STAMP(1);
-  for (int t = 0; t < nk0; ++t) {
+  for (int t = 0; t < nkg; ++t) {
     // K-tile t has landed once at most LPS * (newer stages in flight) loads of this wave are outstanding
-    const int newer = min(NS - 2, nk0 - 1 - t);
+    const int newer = min(NS - 2, nkg - 1 - t);
     switch (newer) {
 #define CMVE_RING_WAIT(k) \
   case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS * (k)) : "memory"); break;
@@ -1411,8 +1428,8 @@ void sim_kernel(
     // every wave's share of K-tile t is in LDS, every wave is done with K-tile t-1 (an LDS-only barrier:
     // __syncthreads would drain vmcnt, i.e. the ring)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (t + NS - 1 < nk0) stage(t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
-    const char* base = smem + (t % NS) * STAGE_BYTES;
+    if (t + NS - 1 < nkg) stage(kt0 + t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
+    const char* base = smem + (group * NS + t % NS) * STAGE_BYTES;
     const char* pA = base;
     const char* pB = base + A_BYTES;
     if constexpr (KSPLIT) {
@@ -1490,6 +1507,31 @@ void sim_kernel(
     }
     if (a.thr_gt && thr_dir) thr_of(sgt_raw, e_raw, tid < BM ? gmax_v : qmax_v, thr_hi_v, thr_lo_v);
     if constexpr (INL) sgt_pub = sgt_raw;  // (after the main loop: the load has been waited for)
+  }
+  if constexpr (KG > 1) {
+    // the second group's partial sums into the first's, through the second group's own (now idle) ring: a barrier
+    // (every wave done reading its ring), group 1 stores, a barrier, group 0 adds; group 1's accumulators become
+    // -inf, which no threshold counts and no band holds (it skips the scoring anyway)
+    static_assert(KG == 2 && NS * STAGE_BYTES >= NT * TM * TN * 16, "the partials fit the second group's ring");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    f32x4_t* part = (f32x4_t*)(smem + NS * STAGE_BYTES) + (size_t)(lw * 64 + lane) * (TM * TN);
+    if (group == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) part[i * TN + j] = acc[i][j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (group == 0) {
+          acc[i][j] += part[i * TN + j];
+        } else {
+          acc[i][j] = f32x4_t{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        }
+      }
   }
   CMVE_STAMP(2);
   } else {
@@ -1583,13 +1625,15 @@ static void geo_fill(SimArgs& a, int64_t nq_pad, int64_t ng_pad, int bm, int bn)
   a.gn = CMVE_SIM_GN;
 }
 
-template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED>
+template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, int KG = 1>
 static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = ring_lds_bytes<MODE, G::BM, G::BN, PHASED, G::NW>();  // + the static epilogue scratch (EpiLds)
+  // + the static epilogue scratch (EpiLds); KG = 2: a ring per K group
+  const size_t lds = ring_lds_bytes<MODE, G::BM, G::BN, PHASED, G::NW>() * KG;
   // once per instantiation; function-local static init is thread-safe (one host thread per shard / GPU)
-  static const hipError_t attr_err = hipFuncSetAttribute((const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED>,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const hipError_t attr_err = hipFuncSetAttribute(
+      (const void*)sim_kernel<MODE, EPI, WM, WN, TM, PHASED, false, KG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)lds);
   CMVE_HIP(attr_err);
   geo_fill(a, nq_pad, ng_pad, G::BM, G::BN);
   unsigned nblocks = (unsigned)a.nblk_m * (unsigned)a.nblk_n;
@@ -1597,8 +1641,8 @@ static int launch_geo(SimArgs a, int64_t nq_pad, int64_t ng_pad, hipStream_t str
     const int cus = std::max(8, device_cus() / 8 * 8);
     nblocks = std::min<unsigned>(nblocks, (unsigned)cus);
   }
-  cmve::launch(sim_kernel<MODE, EPI, WM, WN, TM, PHASED>, dim3(nblocks), dim3(G::NT), (uint32_t)lds, stream, a,
-               (const SimArgs*)nullptr);
+  cmve::launch(sim_kernel<MODE, EPI, WM, WN, TM, PHASED, false, KG>, dim3(nblocks), dim3(G::NT * KG), (uint32_t)lds,
+               stream, a, (const SimArgs*)nullptr);
   return check_launch("sim_kernel");
 }
 
@@ -1634,6 +1678,12 @@ static int launch_sim(const SimArgs& a, int64_t nq_pad, int64_t ng_pad, hipStrea
   // 1.2 us per tile in the K14 stamps); the main loop stays at ~6.3 us (the CU's L2 -> LDS fill of 256 KiB)
   if (force != 128 && (nq_pad / 128) * (ng_pad / 128) < 128 && nq_pad % 64 == 0 && ng_pad % 64 == 0) {
 #ifndef CMVE_G64_2W
+    // the rank GEMM at this size (one K14 evaluation, cmve_rank_mfma of a 1k x 1k problem): its 256 tiles are one per
+    // CU, each a latency chain of 16 K-tiles -- two K groups of 4 waves halve the chain (and share the K14 level-2
+    // re-score): one evaluation 31.6 -> 29.2 us back to back (profiles/r06_ab_g64_kg2.txt).  Every G64 rank launch
+    // takes it, so the separate-launch path and cmve_eval_ranks still see the same scores (CMVE_G64_KG = 1: off)
+    if constexpr (EPI == EPI_RANK && MODE != CMVE_SIM_BF16X3 && CMVE_G64_KG == 2)
+      if (a.nk0 >= 2 && a.nk0 % 2 == 0) return launch_geo<MODE, EPI, 4, 1, 1, false, 2>(a, nq_pad, ng_pad, stream);
     return launch_geo<MODE, EPI, 4, 1, 1, false>(a, nq_pad, ng_pad, stream);
 #else
     return launch_geo<MODE, EPI, 2, 1, 2, false>(a, nq_pad, ng_pad, stream);

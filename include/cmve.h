@@ -432,7 +432,9 @@ int cmve_eval_kernel_timing(cmve_handle_t h, int32_t slot, float* ms4);
  * launch, each over (the blocks of one evaluation) x (the evaluations): a 1,000 x 1,000 evaluation's launches
  * leave most of the chip idle, a batch fills it.  The argument blocks are built and copied to the device at
  * create time (every pointer is baked in: refill the raw rows in place between runs, as for the graph form);
- * run enqueues the three launches on h's stream; the results equal cmve_eval_ranks' bit for bit.  Batches take
+ * run enqueues the three launches on h's stream; the ranks and every R@K / overflow / pairing word equal
+ * cmve_eval_ranks' (out[8] and out[12], the band-pair diagnostics, may differ by a few pairs: one evaluation's
+ * G64 rank GEMM sums K in two halves, a batch's tile in one chain).  Batches take
  * the small-problem geometry (fewer than 128 tiles of 128^2, e.g. 1,000 x 1,000) with the rank GEMM's inline fp64
  * re-score (no overflow); the batch's rank GEMM runs 128 x 128 tiles (split-bf16: 128 x 64), each XCD taking a
  * contiguous run of the (evaluation, tile) pairs.

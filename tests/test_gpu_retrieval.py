@@ -729,6 +729,18 @@ def test_paired_prep_equals_general_prep(torch_cuda, dt):
     assert r1[3] == n
 
 
+
+def _assert_same_results(out, ref):
+    """A batch evaluation against the same evaluation run alone: every output word but the band-pair diagnostics.
+    One evaluation's G64 rank GEMM sums K in two halves (two wave groups, sim.hip KG = 2), a batch's 128 x 128 tile in
+    one chain, so a pair at a band edge may fall on the other side of a threshold: out[8] (band pairs) and out[12]
+    (level-3 pairs) may differ by a few; ranks, R@K, rank sums, the overflow and pairing words may not."""
+    import torch
+    keep = torch.ones_like(ref, dtype=torch.bool)
+    keep[8] = keep[12] = False
+    assert torch.equal(out[keep], ref[keep]), (out[:16].tolist(), ref[:16].tolist())
+    assert abs(int(out[8]) - int(ref[8])) <= 16 and abs(int(out[12]) - int(ref[12])) <= 16
+
 @pytest.mark.parametrize("case", ["c1_paired_f64", "multi_gt_f32", "multi_gt_f32_bf16", "multi_gt_f32_bf16x3"])
 def test_rank_batch_equals_sessions(golden, torch_cuda, case):
     """RankBatch (cmve_eval_batch_*: one prep, one rank GEMM, one finish launch over several evaluations)
@@ -771,8 +783,8 @@ def test_rank_batch_equals_sessions(golden, torch_cuda, case):
     for _ in range(2):
         b.run()
         torch.cuda.synchronize()
-        for s, r in zip(sess, ref):  # every word, out[12] (the level-3 pairs listed) included
-            assert torch.equal(s.out, r), (s.out[:16].tolist(), r[:16].tolist())
+        for s, r in zip(sess, ref):
+            _assert_same_results(s.out, r)
     if case == "c1_paired_f64":
         g = golden("retrieval_c1")
         h = sess[0].out.cpu().numpy()
@@ -781,7 +793,7 @@ def test_rank_batch_equals_sessions(golden, torch_cuda, case):
     sets[1][1].copy_(sets[2][1])
     b.run()
     torch.cuda.synchronize()
-    assert torch.equal(sess[1].out, ref[2])
+    _assert_same_results(sess[1].out, ref[2])
     b.close()
 
 
@@ -919,7 +931,7 @@ def test_rank_batch_dense_tiles(torch_cuda, case):
     torch.cuda.synchronize()
     for s_, r_, (er, ec) in zip(sess, ref, exp):
         h = s_.out.cpu().numpy()
-        assert torch.equal(s_.out[:12], r_[:12]) and torch.equal(s_.out[13:], r_[13:])  # (out[12]: see above)
+        _assert_same_results(s_.out, r_)
         assert h[9] == 0 and h[8] > 4 * 1024  # no overflow; the dense tiles went past the LDS list
         assert np.array_equal(h[16:16 + n], er) and np.array_equal(h[16 + n:], ec)
     b.close()
