@@ -15,7 +15,7 @@ import sys
 # instantiation of the same template and must not be mixed in
 def is_g256_rank(name):
     return "sim_kernel" in name and ("<2, 1, 2, 4, 8, true>" in name or "<2, 1, 2, 4, 8, true, false>" in name
-                                     or "ILi2ELi1ELi2ELi4ELi8ELb1E" in name)
+                                     or "<2, 1, 2, 4, 8, true, false, 1>" in name or "ILi2ELi1ELi2ELi4ELi8ELb1E" in name)
 
 
 def rows(pattern):

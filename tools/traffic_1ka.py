@@ -29,7 +29,8 @@ def role(name):
     """The evaluation launch a kernel name is; the batch kernels (cmve_eval_batch_*: the headline's timed loop)
     and the single-evaluation kernels (cmve_eval_ranks: the bench's latency measurements) are kept apart, so a
     profile holding both never averages one into the other."""
-    batch = "_batch_kernel" in name or ("sim_kernel<2, 1" in name and ", true>" in name)
+    # sim_kernel<MODE, EPI, WM, WN, TM, PHASED, BATCH, KG> (round 6 added KG; earlier traces end at BATCH)
+    batch = "_batch_kernel" in name or ("sim_kernel<2, 1" in name and (", true>" in name or ", true, 1>" in name))
     if "eval_prep_kernel" in name or "eval_prep_pair_kernel" in name or "eval_prep_pair_batch_kernel" in name \
             or "eval_prep_fin_batch_kernel" in name \
             or "eval_prep_batch_kernel" in name or "eval_prep_pair_f16_kernel" in name \
