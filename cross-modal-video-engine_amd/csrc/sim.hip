@@ -48,6 +48,9 @@
 #ifndef CMVE_EVAL_L3_LIST
 #define CMVE_EVAL_L3_LIST 0  // 1: one evaluation lists its level-3 pairs for the finish as batches do
 #endif
+#ifndef CMVE_L2_PIPE
+#define CMVE_L2_PIPE 1  // K14 level-2 re-score: one pair per wave per step, the next pair's rows in flight (0: rounds
+#endif                  // of CMVE_L2_P* pairs per wave, each round one round trip)
 #ifndef CMVE_G64_KG
 #define CMVE_G64_KG 2  // one K14 evaluation's G64 rank GEMM: K groups (2: split-K over two groups of 4 waves)
 #endif
@@ -950,6 +953,75 @@ void sim_kernel(
               // direction left undecided goes to the level-3 list (fp64 in the finish launch, off this kernel's
               // critical path), or -- the list full -- keeps those flags for the fp64 pass below (the wave owns its
               // entries: no other wave touches them)
+#if CMVE_L2_PIPE
+              // software-pipelined: each wave scores one listed pair per step while the rows of its next pair are
+              // already in flight (two pairs' rows in registers, as two pairs per round trip were; the same
+              // arithmetic per pair, so the same bits)
+              struct L2Stage {
+                uint32_t ent;
+                int64_t qr, gc;
+                float elq, elg;
+                L16Frag fq, fg;
+              };
+              auto l2_fetch = [&](int p, L2Stage& st) {
+                st.ent = epi.list[p];
+                st.qr = m0 + (st.ent & 0xff);
+                st.gc = n0 + ((st.ent >> 8) & 0xff);
+                st.elq = gld(a.q_el + st.qr);  // (the row bounds travel with the plane rows)
+                st.elg = gld(a.g_el + st.gc);
+                const int64_t k = 16 * (int64_t)lane;  // (the level-2 planes need d_pad <= 1024: one chunk)
+                if (k < a.ldk) {
+                  l16_load(a.qhi + st.qr * a.ldk, a.q_lo16 + st.qr * a.ldk, k, st.fq);
+                  l16_load(a.ghi + st.gc * a.ldk, a.g_lo16 + st.gc * a.ldk, k, st.fg);
+                }
+              };
+              auto l2_finish = [&](int p, const L2Stage& st) {
+                double s2 = 16 * (int64_t)lane < a.ldk ? l16_partial(st.fq, st.fg, 0.0) : 0.0;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+                if (lane == 0) {
+                  const double eq = (double)st.elq, eg = (double)st.elg;
+                  const double E2 = eq + (1.0 + eq) * eg + 2e-12;
+                  uint32_t fl = (st.ent >> 16) & 3u;
+                  const int lr = (int)(st.ent & 0xff), lc = (int)((st.ent >> 8) & 0xff);
+                  if (fl & 1u) {
+                    const double t = epi.sgt[lr];
+                    if (s2 - E2 > t) { lds_add_u32_async(&lds_rc[lr], 1); fl &= ~1u; }
+                    else if (s2 + E2 < t) fl &= ~1u;
+                  }
+                  if (fl & 2u) {
+                    const double t = epi.sgt[BM + lc];
+                    if (s2 - E2 > t) { lds_add_u32_async(&lds_cc[lc], 1); fl &= ~2u; }
+                    else if (s2 + E2 < t) fl &= ~2u;
+                  }
+                  if (fl && a.l3_count) {  // level 3: counted (a returning atomic: only these few pairs pay it),
+                    const unsigned slot = gadd(a.l3_count, 1u);  // listed for the finish (batches) or, with no
+                    if (a.l3 && slot < (unsigned)a.l3_cap) {     // list (one evaluation), re-scored right here
+                      gst(a.l3 + slot, (unsigned long long)st.qr | ((unsigned long long)st.gc << 31) |
+                                           ((unsigned long long)fl << 62));
+                      fl = 0u;
+                    }
+                  }
+                  epi.list[p] = (st.ent & 0xffffu) | (fl << 16);
+                }
+              };
+              {
+                L2Stage sa, sb;
+                int p = wave;
+                if (p < ntot) l2_fetch(p, sa);
+                while (p < ntot) {  // (two named stages, no register copies)
+                  int pn = p + NWT;
+                  if (pn < ntot) l2_fetch(pn, sb);
+                  l2_finish(p, sa);
+                  p = pn;
+                  if (p >= ntot) break;
+                  pn = p + NWT;
+                  if (pn < ntot) l2_fetch(pn, sa);
+                  l2_finish(p, sb);
+                  p = pn;
+                }
+              }
+#else
               constexpr int RP = BATCH ? ((is_big_ring<BM, BN>() || NW == 4) ? CMVE_L2_P_BIG : CMVE_L2_P) : CMVE_L2_P_ONE;
               for (int p0 = wave * RP; p0 < ntot; p0 += NWT * RP) {
                 int64_t qr[RP], gc[RP];
@@ -1000,6 +1072,7 @@ void sim_kernel(
                   }
                 }
               }
+#endif
               CMVE_BAR_LDS();  // the level-2 flags are in LDS for every wave
             }
             auto rescore2 = [&](uint32_t e1, uint32_t e2, bool two) {
