@@ -190,27 +190,37 @@ __device__ __forceinline__ void tile_grouped(int L, int nblk_m, int nblk_n, int 
 // (KB = 64, 8 chunks) XOR the row's low 3 bits; 64-B rows (KB = 32, 4 chunks, four rows per 256-B bank line) XOR
 // bits 2-3, so rows r, r + 4, r + 8, r + 12 of one bank offset take four different slots
 template <int KB>
-__device__ __forceinline__ int lds_swz(int r) {
+__host__ __device__ constexpr int lds_swz(int r) {
   return KB == 64 ? (r & 7) : ((r >> 2) & 3);
 }
 
-// issue this wave's share of one ROWS x KB (bf16/fp16) plane: ROWS x 2KB / 1 KiB wave-instructions of 1 KiB
+// this lane's byte offset inside any staging wave-instruction of a KB-deep K-tile: one instruction's 64 lanes cover
+// RPI whole rows, and the swizzle takes only a row's low bits (KB = 64: r & 7 with RPI = 8; KB = 32: (r >> 2) & 3
+// with RPI = 16), so the offset is the same for every instruction of every wave -- computed once per kernel, the K
+// loop's staging is scalar address math (per-instruction 64-bit lane address math cost ~60 VALU cycles x 8 per wave
+// per K-tile in the batch ring)
+template <int KB>
+__device__ __forceinline__ uint32_t stage_lane_off(int64_t ldk, int lane) {
+  constexpr int CPR = KB / 8;  // 16-B chunks per row
+  const int r = lane / CPR, c = lane % CPR;
+  return (uint32_t)(((int64_t)r * ldk + (c ^ lds_swz<KB>(r)) * 8) * 2);
+}
+
+// issue this wave's share of one ROWS x KB (bf16/fp16) plane: ROWS x 2KB / 1 KiB wave-instructions of 1 KiB; src,
+// ldk, row0, k0 and wave are uniform (the block base is scalar; loff = stage_lane_off<KB>)
 template <int ROWS, int NW, int KB = BK>
 __device__ __forceinline__ void stage_plane(const uint16_t* __restrict__ src, int64_t ldk, int row0, int k0,
-                                            char* lds_plane, int wave, int lane) {
+                                            char* lds_plane, int wave, uint32_t loff) {
   constexpr int CPR = KB / 8;    // 16-B chunks per row
   constexpr int RPI = 64 / CPR;  // rows per wave-instruction
   constexpr int PER_WAVE = ROWS / RPI / NW;
   static_assert(PER_WAVE * RPI * NW == ROWS, "plane rows must split evenly over the waves");
+  static_assert(lds_swz<KB>(RPI) == 0 && lds_swz<KB>(RPI - 1) == lds_swz<KB>(2 * RPI - 1), "swizzle period");
+  const char* blk = (const char*)(src + ((int64_t)row0 + wave * PER_WAVE * RPI) * ldk + k0);
 #pragma unroll
-  for (int it = 0; it < PER_WAVE; ++it) {
-    const int chunk = wave * PER_WAVE + it;
-    const int r = chunk * RPI + lane / CPR;
-    const int c = lane % CPR;
-    const int gc = c ^ lds_swz<KB>(r);
-    const uint16_t* g = src + (int64_t)(row0 + r) * ldk + k0 + gc * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void_t*)(lds_plane + chunk * 1024), 16, 0, 0);
-  }
+  for (int it = 0; it < PER_WAVE; ++it)
+    __builtin_amdgcn_global_load_lds((const void*)(blk + (int64_t)it * RPI * ldk * 2 + loff),
+                                     (lds_void_t*)(lds_plane + (wave * PER_WAVE + it) * 1024), 16, 0, 0);
 }
 
 template <int KB = BK>
@@ -572,17 +582,25 @@ void sim_kernel(
     if (PHASED || !a.thr_gt) fetch_thr(m0, n0, thr_hi_v, thr_lo_v);
   }
 
+  // the staging operands held in registers: a batch's `a` lives in device memory, and the compiler re-read these
+  // fields (a scalar round trip) around the LDS-DMA issues of every K-tile
+  const uint16_t* const st_qhi = a.qhi;
+  const uint16_t* const st_ghi = a.ghi;
+  const uint16_t* const st_qlo = MODE == CMVE_SIM_BF16X3 ? a.qlo : nullptr;
+  const uint16_t* const st_glo = MODE == CMVE_SIM_BF16X3 ? a.glo : nullptr;
+  const int64_t st_ldk = a.ldk;
+  const uint32_t st_loff = stage_lane_off<KB>(st_ldk, lane);
   auto stage = [&](int t, int s) {
 #ifdef CMVE_DBG_NOLOAD
     return;
 #endif
     char* base = smem + (group * NS + s) * STAGE_BYTES;  // (KG = 2: each group's ring of its own)
     const int k0 = t * KB;
-    stage_plane<BM, NW, KB>(a.qhi, a.ldk, m0, k0, base, lw, lane);
-    stage_plane<BN, NW, KB>(a.ghi, a.ldk, n0, k0, base + A_BYTES, lw, lane);
+    stage_plane<BM, NW, KB>(st_qhi, st_ldk, m0, k0, base, lw, st_loff);
+    stage_plane<BN, NW, KB>(st_ghi, st_ldk, n0, k0, base + A_BYTES, lw, st_loff);
     if (MODE == CMVE_SIM_BF16X3) {
-      stage_plane<BM, NW, KB>(a.qlo, a.ldk, m0, k0, base + A_BYTES + B_BYTES, lw, lane);
-      stage_plane<BN, NW, KB>(a.glo, a.ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, lw, lane);
+      stage_plane<BM, NW, KB>(st_qlo, st_ldk, m0, k0, base + A_BYTES + B_BYTES, lw, st_loff);
+      stage_plane<BN, NW, KB>(st_glo, st_ldk, n0, k0, base + 2 * A_BYTES + B_BYTES, lw, st_loff);
     }
   };
 
