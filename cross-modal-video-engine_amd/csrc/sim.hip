@@ -54,6 +54,11 @@
 #ifndef CMVE_G64_KG
 #define CMVE_G64_KG 2  // one K14 evaluation's G64 rank GEMM: K groups (2: split-K over two groups of 4 waves)
 #endif
+#ifndef CMVE_RING_READS_FIRST
+// ring loops: a K-tile's fragment reads all issued before its MFMAs (study: the batch rank GEMM alone 41.0 -> 38.4 us,
+// one stream 8.5 -> 8.65e10, but three streams 1.26 -> 1.20e11 -- profiles/r06_ab_reads_first.txt)
+#define CMVE_RING_READS_FIRST 0
+#endif
 
 namespace cmve {
 
@@ -383,7 +388,7 @@ constexpr size_t ring_lds_bytes() {
 // scalar branches and stores cost it SGPR spills at the 256-VGPR cap)
 #define CMVE_STAMP(k) \
   if constexpr (!PHASED) {  \
-    if (a.dbg_stamps && threadIdx.x == 0) a.dbg_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (a.dbg_stamps && threadIdx.x == 0) gst(a.dbg_stamps + (size_t)tile * 8 + (k), __builtin_amdgcn_s_memrealtime()); \
   }
 #endif
 
@@ -448,6 +453,11 @@ struct EpiLds<BM, BN, false, INL> {
 #ifndef CMVE_BATCH_WPE
 #define CMVE_BATCH_WPE 4  // the batch ring kernels: waves per SIMD the register budget must allow (<= 128 VGPRs)
 #endif
+#ifndef CMVE_BATCH4_WPE
+// the default 4-wave 128 x 128 batch tile: 3 waves per SIMD (<= 168 VGPRs) -- two GEMM blocks per CU and a wave of
+// another stream's prep beside them on every SIMD (the product kernel needs 152)
+#define CMVE_BATCH4_WPE 3
+#endif
 // KG = 2 (one K14 evaluation's G64 rank GEMM, sim_kernel_kg2): two groups of WM x WN waves, each streaming half of
 // the K-tiles through a ring of its own; the second group's partial sums are added to the first's through LDS
 // before the epilogue (every output element: two fp32 MFMA chains of d/2 then one fp32 add -- inside the same error
@@ -455,7 +465,10 @@ struct EpiLds<BM, BN, false, INL> {
 template <int MODE, int EPI, int WM, int WN, int TM, bool PHASED, bool BATCH = false, int KG = 1>
 __global__ __launch_bounds__(WM * WN * 64 * KG,
                             KG > 1 ? 1
-                                   : (BATCH ? ((is_big_ring<WM * TM * 16, WN * 64>() || WM * WN == 4) ? 2 : CMVE_BATCH_WPE)
+                                   : (BATCH ? (is_big_ring<WM * TM * 16, WN * 64>()
+                                                   ? 2
+                                                   : (WM * WN == 4 ? (MODE == CMVE_SIM_BF16X3 ? 2 : CMVE_BATCH4_WPE)
+                                                                   : CMVE_BATCH_WPE))
                                             : ((WM * TM * 16 == 64 && WN == 1) ? CMVE_G64_BLOCKS : 2)))
 void sim_kernel(
     SimArgs a_arg, const SimArgs* __restrict__ tab) {
@@ -541,17 +554,17 @@ void sim_kernel(
     hi = lo = __builtin_nanf("");
     if (tid < BM) {
       if (a.row_hi) {
-        if (!PHASED && a.thr_gt) thr_of(a.row_sgt[mo + tid], a.q_err[mo + tid], gmax_v, hi, lo);
+        if (!PHASED && a.thr_gt) thr_of(gld(a.row_sgt + mo + tid), gld(a.q_err + mo + tid), gmax_v, hi, lo);
         else {
-          hi = a.row_hi[mo + tid];
-          lo = a.row_lo[mo + tid];
+          hi = gld(a.row_hi + mo + tid);
+          lo = gld(a.row_lo + mo + tid);
         }
       }
     } else if (tid < BM + BN && a.col_hi) {
-      if (!PHASED && a.thr_gt) thr_of(a.col_sgt[no + tid - BM], a.g_err[no + tid - BM], qmax_v, hi, lo);
+      if (!PHASED && a.thr_gt) thr_of(gld(a.col_sgt + no + tid - BM), gld(a.g_err + no + tid - BM), qmax_v, hi, lo);
       else {
-        hi = a.col_hi[no + tid - BM];
-        lo = a.col_lo[no + tid - BM];
+        hi = gld(a.col_hi + no + tid - BM);
+        lo = gld(a.col_lo + no + tid - BM);
       }
     }
   };
@@ -1519,6 +1532,11 @@ void sim_kernel(
     // every wave's share of K-tile t is in LDS, every wave is done with K-tile t-1 (an LDS-only barrier:
     // __syncthreads would drain vmcnt, i.e. the ring)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if CMVE_RING_READS_FIRST
+    // the same drain as a builtin the compiler's wait-count pass sees: with a scalar load it believes outstanding
+    // (the asm above is opaque to it) every LDS-read wait below would be lgkmcnt(0) instead of counted
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left at their maxima (gfx9 encoding)
+#endif
     if (t + NS - 1 < nkg) stage(kt0 + t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
     const char* base = smem + (group * NS + t % NS) * STAGE_BYTES;
     const char* pA = base;
@@ -1549,6 +1567,12 @@ void sim_kernel(
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[ks][i] = read_frag<KB>(pA, wr * (TM * 16) + i * 16 + frow, chunk);
     }
+#if CMVE_RING_READS_FIRST
+    // every fragment read of the K-tile issued before its first MFMA: each 32-deep step's MFMAs wait (counted
+    // lgkmcnt) only for their own reads, the later step's reads land under the earlier step's MFMAs (left to the
+    // scheduler, the reads went out in groups of 6 and 2, each drained by lgkmcnt(0) right before its MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if constexpr (MODE == CMVE_SIM_BF16X3) {  // pairs (lo, hi) then (hi, lo): plane_of's order
       const char* pAl = base + A_BYTES + B_BYTES;
       const char* pBl = base + 2 * A_BYTES + B_BYTES;
@@ -1578,12 +1602,22 @@ void sim_kernel(
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], lx[ks][j], acc[i][j]);
     }
+#ifdef CMVE_DBG_NOMFMA  // diagnostic build only: the fragments are read, no MFMA issued (results garbage)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[ks][i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[ks][j]));
+    }
+#else
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the threshold loads, if any are still out)
   if constexpr (epi_thr(EPI)) {
