@@ -951,6 +951,9 @@ __global__ __launch_bounds__(PREP_NT, CMVE_PREPFIN_WPE) void eval_prep_fin_batch
                                                                                     const EvalItem* __restrict__ ftab,
                                                                                     int nprep, int nfin) {
   static_assert(PREP_NT == FIN_NT, "one block size for both roles");
+#ifdef CMVE_STUDY_PREP_PRIO  // study: the chained prep's waves at a raised priority beside another stream's rank GEMM
+  __builtin_amdgcn_s_setprio(CMVE_STUDY_PREP_PRIO);
+#endif
   if ((int)blockIdx.x < nprep) {
     const EvalItem& it = ptab[blockIdx.y];
     eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c, blockIdx.x, nprep);

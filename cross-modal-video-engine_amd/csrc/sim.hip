@@ -1518,6 +1518,9 @@ void sim_kernel(
     }
   }
   CMVE_STAMP(1);
+#ifdef CMVE_STUDY_LOOP_PRIO  // study: the batch ring's main loop at a raised wave priority (the co-resident preps' waves
+  if constexpr (BATCH) __builtin_amdgcn_s_setprio(CMVE_STUDY_LOOP_PRIO);  // stay at 0)
+#endif
   for (int t = 0; t < nkg; ++t) {
     // K-tile t has landed once at most LPS * (newer stages in flight) loads of this wave are outstanding
     const int newer = min(NS - 2, nkg - 1 - t);
@@ -1619,6 +1622,9 @@ void sim_kernel(
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
 #endif
   }
+#ifdef CMVE_STUDY_LOOP_PRIO
+  if constexpr (BATCH) __builtin_amdgcn_s_setprio(0);
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the threshold loads, if any are still out)
   if constexpr (epi_thr(EPI)) {
     if (a.thr_gt) {  // fold the shards: a wave max (every lane the same bits)
