@@ -517,15 +517,18 @@ __device__ __forceinline__ void pack_f16_lo16(const EvalSide& A, int64_t row, co
 // one VGPR offset for every load of the row, the 256-element steps in scalar offsets (per-load 64-bit
 // addresses held ~64 registers and pushed the prep past 128)
 typedef uint32_t prep_u32x4 __attribute__((ext_vector_type(4)));
+#ifndef CMVE_PREP_ROW_AUX
+#define CMVE_PREP_ROW_AUX 0  // the raw rows' cache policy (gfx950 buffer aux bits: 2 = nt, 1 = sc0, 16 = sc1)
+#endif
 typedef double prep_f64x2 __attribute__((ext_vector_type(2)));
 template <int NM>
 __device__ __forceinline__ void load_row_buf(const double* row, int lane, double (&v)[NM][4]) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, NM * 256 * 8, 0x00020000);
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    const prep_f64x2 a = __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32, m * 2048, 0));
+    const prep_f64x2 a = __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32, m * 2048, CMVE_PREP_ROW_AUX));
     const prep_f64x2 b =
-        __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32 + 16, m * 2048, 0));
+        __builtin_bit_cast(prep_f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32 + 16, m * 2048, CMVE_PREP_ROW_AUX));
     v[m][0] = a.x;
     v[m][1] = a.y;
     v[m][2] = b.x;
@@ -537,7 +540,7 @@ __device__ __forceinline__ void load_row_buf(const float* row, int lane, double 
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, NM * 256 * 4, 0x00020000);
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    const cmve_f32x4 a = __builtin_bit_cast(cmve_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, m * 1024, 0));
+    const cmve_f32x4 a = __builtin_bit_cast(cmve_f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, m * 1024, CMVE_PREP_ROW_AUX));
     v[m][0] = a.x;
     v[m][1] = a.y;
     v[m][2] = a.z;
