@@ -54,6 +54,9 @@
 #ifndef CMVE_G64_KG
 #define CMVE_G64_KG 2  // one K14 evaluation's G64 rank GEMM: K groups (2: split-K over two groups of 4 waves)
 #endif
+#ifndef CMVE_EPI_BOTH_ASM
+#define CMVE_EPI_BOTH_ASM 1  // rank epilogue, both directions: hand-scheduled scoring (pair2_count_bits); 0: compiler's
+#endif
 #ifndef CMVE_RING_READS_FIRST
 // ring loops: a K-tile's fragment reads all issued before its MFMAs (study: the batch rank GEMM alone 41.0 -> 38.4 us,
 // one stream 8.5 -> 8.65e10, but three streams 1.26 -> 1.20e11 -- profiles/r06_ab_reads_first.txt)
@@ -291,6 +294,44 @@ __device__ __forceinline__ uint32_t row4_count_bits(float s0, float s1, float s2
       : [s0] "v"(s0), [s1] "v"(s1), [s2] "v"(s2), [s3] "v"(s3), [hi] "v"(hi), [lo] "v"(lo), [sh0] "n"(R),
         [sh1] "n"(4 + R), [sh2] "n"(8 + R), [sh3] "n"(12 + R));
   return c;
+}
+
+// Both directions at once (the K14 evaluation's shape): two scores sa, sb of one column block (rows ra, rb of the
+// lane's four) against their row thresholds (hia, loa), (hib, lob) and the column's (chi, clo).  Adds the exact
+// counts #{s > hi} to ca, cb (row) and cc (column) and appends the exact band bits "lo <= s <= hi" (s >= lo and not
+// s > hi: lo <= hi, or both NaN / +inf) to urow / ucol by doubling -- u = 2u + bit is ONE v_addc with the lane mask
+// as carry-in, so the callers feed bits most significant first (j = 3..0, then r = 3..0: bit j * 4 + r).  8 VALU
+// + 2 SALU per score (the compiler's form of the same tests: ~18 VALU).  Every lane mask has its own SGPR pair and
+// is read >= 4 instructions after it is written (row4_count_bits' rule).
+__device__ __forceinline__ void pair2_count_bits(float sa, float sb, float hia, float loa, float hib, float lob,
+                                                 float chi, float clo, uint32_t& ca, uint32_t& cb, uint32_t& cc,
+                                                 uint32_t& urow, uint32_t& ucol) {
+  unsigned long long ma, mb, na, nb, la, lb, ka, kb, cy;
+  asm("v_cmp_gt_f32_e64 %[ma], %[sa], %[hia]\n\t"
+      "v_cmp_gt_f32_e64 %[mb], %[sb], %[hib]\n\t"
+      "v_cmp_gt_f32_e64 %[na], %[sa], %[chi]\n\t"
+      "v_cmp_gt_f32_e64 %[nb], %[sb], %[chi]\n\t"
+      "v_cmp_ge_f32_e64 %[la], %[sa], %[loa]\n\t"
+      "v_cmp_ge_f32_e64 %[lb], %[sb], %[lob]\n\t"
+      "v_cmp_ge_f32_e64 %[ka], %[sa], %[clo]\n\t"
+      "v_cmp_ge_f32_e64 %[kb], %[sb], %[clo]\n\t"
+      "v_addc_co_u32_e64 %[ca], %[cy], %[ca], 0, %[ma]\n\t"
+      "v_addc_co_u32_e64 %[cb], %[cy], %[cb], 0, %[mb]\n\t"
+      "v_addc_co_u32_e64 %[cc], %[cy], %[cc], 0, %[na]\n\t"
+      "v_addc_co_u32_e64 %[cc], %[cy], %[cc], 0, %[nb]\n\t"
+      "s_andn2_b64 %[la], %[la], %[ma]\n\t"
+      "s_andn2_b64 %[lb], %[lb], %[mb]\n\t"
+      "s_andn2_b64 %[ka], %[ka], %[na]\n\t"
+      "s_andn2_b64 %[kb], %[kb], %[nb]\n\t"
+      "v_addc_co_u32_e64 %[ur], %[cy], %[ur], %[ur], %[la]\n\t"
+      "v_addc_co_u32_e64 %[ur], %[cy], %[ur], %[ur], %[lb]\n\t"
+      "v_addc_co_u32_e64 %[uc], %[cy], %[uc], %[uc], %[ka]\n\t"
+      "v_addc_co_u32_e64 %[uc], %[cy], %[uc], %[uc], %[kb]"
+      : [ca] "+v"(ca), [cb] "+v"(cb), [cc] "+v"(cc), [ur] "+v"(urow), [uc] "+v"(ucol), [ma] "=&s"(ma),
+        [mb] "=&s"(mb), [na] "=&s"(na), [nb] "=&s"(nb), [la] "=&s"(la), [lb] "=&s"(lb), [ka] "=&s"(ka),
+        [kb] "=&s"(kb), [cy] "=&s"(cy)
+      : [sa] "v"(sa), [sb] "v"(sb), [hia] "v"(hia), [loa] "v"(loa), [hib] "v"(hib), [lob] "v"(lob), [chi] "v"(chi),
+        [clo] "v"(clo));
 }
 
 template <int MODE>
@@ -832,6 +873,21 @@ void sim_kernel(
           // pass 3.92 -> 3.83 ms, tools/ab4.sh)
           uint32_t u = 0u;
 #ifndef CMVE_EPI_C
+#if CMVE_EPI_BOTH_ASM
+          if constexpr (DR && DC && TN == 4) {  // both directions (K14 evaluations): hand-scheduled per column block
+            uint32_t ur = 0u, uc = 0u;
+  #pragma unroll
+            for (int j = TN - 1; j >= 0; --j) {  // (bits j * 4 + r, most significant first)
+              pair2_count_bits(acc[i][j][3], acc[i][j][2], rhi[3], rlo[3], rhi[2], rlo[2], chi[j], clo[j], c3, c2,
+                               ccnt[j], ur, uc);
+              pair2_count_bits(acc[i][j][1], acc[i][j][0], rhi[1], rlo[1], rhi[0], rlo[0], chi[j], clo[j], c1, c0,
+                               ccnt[j], ur, uc);
+            }
+            row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+            und[i] = ur | (uc << 16);
+            continue;
+          }
+#endif
           if constexpr (DR && !DC && TN == 4) {  // t2v (the bench / gallery shape): hand-scheduled per row
             c0 = row4_count_bits<0>(acc[i][0][0], acc[i][1][0], acc[i][2][0], acc[i][3][0], rhi[0], rlo[0], u);
             c1 = row4_count_bits<1>(acc[i][0][1], acc[i][1][1], acc[i][2][1], acc[i][3][1], rhi[1], rlo[1], u);
