@@ -57,6 +57,9 @@
 #ifndef CMVE_EPI_BOTH_ASM
 #define CMVE_EPI_BOTH_ASM 1  // rank epilogue, both directions: hand-scheduled scoring (pair2_count_bits); 0: compiler's
 #endif
+#ifndef CMVE_RING_VGPR_STAGE
+#define CMVE_RING_VGPR_STAGE 0  // the batch ring: K-tiles staged through registers instead of LDS-DMA (study)
+#endif
 #ifndef CMVE_RING_READS_FIRST
 // ring loops: a K-tile's fragment reads all issued before its MFMAs (study: the batch rank GEMM alone 41.0 -> 38.4 us,
 // one stream 8.5 -> 8.65e10, but three streams 1.26 -> 1.20e11 -- profiles/r06_ab_reads_first.txt)
@@ -1558,7 +1561,38 @@ void sim_kernel(
       emg = gld(a.g_emax + lane);
     }
   }
-  for (int t = 0; t < NS - 1 && t < nkg; ++t) stage(kt0 + t, t);
+  // CMVE_RING_VGPR_STAGE (the batch ring): K-tiles staged through registers -- global_load_dwordx4 of the same 16 B per
+  // lane an LDS-DMA piece moves, ds_write_b128 into the same LDS image -- one K-tile ahead in registers, one in LDS
+  // (an LDS-DMA piece costs its wave ~100-185 issue cycles inside a phase of MFMAs and fragment reads,
+  // MI355X_MICROARCH.md: 8 per wave per K-tile, the main loop's largest single cost)
+  constexpr bool RSTG = CMVE_RING_VGPR_STAGE && BATCH && MODE != CMVE_SIM_BF16X3 && KG == 1 && NS == 2;
+  constexpr int PWA = RSTG ? BM / RPI / NW : 1, PWB = RSTG ? BN / RPI / NW : 1;
+  cmve_u32x4 stg_a[PWA], stg_b[PWB];
+  auto rload = [&](int t) {
+    const int k0 = t * KB;
+    const char* ba = (const char*)(st_qhi + ((int64_t)m0 + lw * PWA * RPI) * st_ldk + k0);
+    const char* bb = (const char*)(st_ghi + ((int64_t)n0 + lw * PWB * RPI) * st_ldk + k0);
+#pragma unroll
+    for (int it = 0; it < PWA; ++it) stg_a[it] = gld((const cmve_u32x4*)(ba + (int64_t)it * RPI * st_ldk * 2 + st_loff));
+#pragma unroll
+    for (int it = 0; it < PWB; ++it) stg_b[it] = gld((const cmve_u32x4*)(bb + (int64_t)it * RPI * st_ldk * 2 + st_loff));
+  };
+  auto rstore = [&](int s) {
+    char* base = smem + s * STAGE_BYTES;
+#pragma unroll
+    for (int it = 0; it < PWA; ++it) *(cmve_u32x4*)(base + (lw * PWA + it) * 1024 + lane * 16) = stg_a[it];
+#pragma unroll
+    for (int it = 0; it < PWB; ++it) *(cmve_u32x4*)(base + A_BYTES + (lw * PWB + it) * 1024 + lane * 16) = stg_b[it];
+  };
+  if constexpr (RSTG) {
+    if (nkg > 0) {
+      rload(kt0);
+      rstore(0);
+    }
+    if (nkg > 1) rload(kt0 + 1);
+  } else {
+    for (int t = 0; t < NS - 1 && t < nkg; ++t) stage(kt0 + t, t);
+  }
   // K14 thresholds: the GT score / bound loads are issued behind the first K-tiles' loads and the rule
   // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
   double sgt_raw = 0.0;
@@ -1579,8 +1613,9 @@ void sim_kernel(
 #endif
   for (int t = 0; t < nkg; ++t) {
     // K-tile t has landed once at most LPS * (newer stages in flight) loads of this wave are outstanding
-    const int newer = min(NS - 2, nkg - 1 - t);
+    const int newer = RSTG ? -1 : min(NS - 2, nkg - 1 - t);  // (RSTG: K-tile t is in LDS, its loads long waited for)
     switch (newer) {
+      case -1: break;
 #define CMVE_RING_WAIT(k) \
   case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS * (k)) : "memory"); break;
       CMVE_RING_WAIT(0) CMVE_RING_WAIT(1) CMVE_RING_WAIT(2) CMVE_RING_WAIT(3) CMVE_RING_WAIT(4) CMVE_RING_WAIT(5)
@@ -1596,7 +1631,8 @@ void sim_kernel(
     // (the asm above is opaque to it) every LDS-read wait below would be lgkmcnt(0) instead of counted
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left at their maxima (gfx9 encoding)
 #endif
-    if (t + NS - 1 < nkg) stage(kt0 + t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
+    if constexpr (!RSTG)
+      if (t + NS - 1 < nkg) stage(kt0 + t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
     const char* base = smem + (group * NS + t % NS) * STAGE_BYTES;
     const char* pA = base;
     const char* pB = base + A_BYTES;
@@ -1677,6 +1713,12 @@ void sim_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma<MODE>(fa[ks][i], fb[ks][j], acc[i][j]);
 #endif
+    if constexpr (RSTG) {  // K-tile t+1 into the other buffer (read by every wave before the barrier above), t+2 loaded
+      if (t + 1 < nkg) {
+        rstore((t + 1) % NS);
+        if (t + 2 < nkg) rload(kt0 + t + 2);
+      }
+    }
   }
 #ifdef CMVE_STUDY_LOOP_PRIO
   if constexpr (BATCH) __builtin_amdgcn_s_setprio(0);
