@@ -57,6 +57,9 @@
 #ifndef CMVE_EPI_BOTH_ASM
 #define CMVE_EPI_BOTH_ASM 1  // rank epilogue, both directions: hand-scheduled scoring (pair2_count_bits); 0: compiler's
 #endif
+#ifndef CMVE_RING_KROT
+#define CMVE_RING_KROT 0  // the batch ring: K-slice order rotated per tile (study)
+#endif
 #ifndef CMVE_RING_VGPR_STAGE
 #define CMVE_RING_VGPR_STAGE 0  // the batch ring: K-tiles staged through registers instead of LDS-DMA (study)
 #endif
@@ -1550,6 +1553,15 @@ void sim_kernel(
   const int nk0 = a.nk0 * (BK / KB);  // (a.nk0: 64-deep K-tiles; d_pad % 64 == 0)
   // KG = 2: this wave's group streams K-tiles [kt0, kt0 + nkg) (the host launches it only for nk0 % 2 == 0)
   const int nkg = nk0 / KG, kt0 = group * nkg;
+  // the K-tile streamed at step t: in order, or (CMVE_RING_KROT study) rotated per tile, so the tiles of an XCD that
+  // run in lockstep read different K-slices of their shared panels at any moment (each tile's own sum in another
+  // order: the scores move within the error bound, the ranks do not)
+#if CMVE_RING_KROT
+  const int krot = BATCH ? (int)(((unsigned)(m0 / BM) * 3u + (unsigned)(n0 / BN) * 5u) % (unsigned)max(nkg, 1)) : 0;
+  auto kt_of = [&](int t) { const int u = t + krot; return kt0 + (u >= nkg ? u - nkg : u); };
+#else
+  auto kt_of = [&](int t) { return kt0 + t; };
+#endif
   // K14: the other set's err_max shards as VECTOR loads, one shard per lane, issued before the first
   // K-tiles (the oldest loads: retired by the first ring wait) and folded after the main loop -- as scalar
   // loads their round trip held the prologue (~2.5 us to the first K-tile in the stamps)
@@ -1591,7 +1603,7 @@ void sim_kernel(
     }
     if (nkg > 1) rload(kt0 + 1);
   } else {
-    for (int t = 0; t < NS - 1 && t < nkg; ++t) stage(kt0 + t, t);
+    for (int t = 0; t < NS - 1 && t < nkg; ++t) stage(kt_of(t), t);
   }
   // K14 thresholds: the GT score / bound loads are issued behind the first K-tiles' loads and the rule
   // applied after the main loop (using them at once would wait vmcnt(0), i.e. for every staged K-tile)
@@ -1632,7 +1644,7 @@ void sim_kernel(
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt left at their maxima (gfx9 encoding)
 #endif
     if constexpr (!RSTG)
-      if (t + NS - 1 < nkg) stage(kt0 + t + NS - 1, (t + NS - 1) % NS);  // refills K-tile t-1's buffer
+      if (t + NS - 1 < nkg) stage(kt_of(t + NS - 1), (t + NS - 1) % NS);  // refills K-tile t-1's buffer
     const char* base = smem + (group * NS + t % NS) * STAGE_BYTES;
     const char* pA = base;
     const char* pB = base + A_BYTES;
