@@ -57,6 +57,9 @@
 #ifndef CMVE_EPI_BOTH_ASM
 #define CMVE_EPI_BOTH_ASM 1  // rank epilogue, both directions: hand-scheduled scoring (pair2_count_bits); 0: compiler's
 #endif
+#ifndef CMVE_EPI_T2V_DBL
+#define CMVE_EPI_T2V_DBL 0  // rank epilogue, t2v only: col4_count_bits (band bits by doubling) instead of row4_count_bits
+#endif
 #ifndef CMVE_RING_KROT
 #define CMVE_RING_KROT 0  // the batch ring: K-slice order rotated per tile (study)
 #endif
@@ -338,6 +341,40 @@ __device__ __forceinline__ void pair2_count_bits(float sa, float sb, float hia, 
         [kb] "=&s"(kb), [cy] "=&s"(cy)
       : [sa] "v"(sa), [sb] "v"(sb), [hia] "v"(hia), [loa] "v"(loa), [hib] "v"(hib), [lob] "v"(lob), [chi] "v"(chi),
         [clo] "v"(clo));
+}
+
+// t2v only (the gallery shape): the four scores of one column block (rows r = 3..0 of the lane's four) against
+// their row thresholds; the counts go to c3..c0 and the band bits are appended to u by doubling (bit j * 4 + r, most
+// significant first, as pair2_count_bits): 4 VALU + 1 SALU per score (row4_count_bits: 5 + 1)
+__device__ __forceinline__ void col4_count_bits(float s3, float s2, float s1, float s0, const f32x4_t& hi,
+                                                const f32x4_t& lo, uint32_t& c3, uint32_t& c2, uint32_t& c1,
+                                                uint32_t& c0, uint32_t& u) {
+  unsigned long long m3, m2, m1, m0, l3, l2, l1, l0, cy;
+  asm("v_cmp_gt_f32_e64 %[m3], %[s3], %[h3]\n\t"
+      "v_cmp_gt_f32_e64 %[m2], %[s2], %[h2]\n\t"
+      "v_cmp_gt_f32_e64 %[m1], %[s1], %[h1]\n\t"
+      "v_cmp_gt_f32_e64 %[m0], %[s0], %[h0]\n\t"
+      "v_cmp_ge_f32_e64 %[l3], %[s3], %[o3]\n\t"
+      "v_cmp_ge_f32_e64 %[l2], %[s2], %[o2]\n\t"
+      "v_cmp_ge_f32_e64 %[l1], %[s1], %[o1]\n\t"
+      "v_cmp_ge_f32_e64 %[l0], %[s0], %[o0]\n\t"
+      "v_addc_co_u32_e64 %[c3], %[cy], %[c3], 0, %[m3]\n\t"
+      "v_addc_co_u32_e64 %[c2], %[cy], %[c2], 0, %[m2]\n\t"
+      "v_addc_co_u32_e64 %[c1], %[cy], %[c1], 0, %[m1]\n\t"
+      "v_addc_co_u32_e64 %[c0], %[cy], %[c0], 0, %[m0]\n\t"
+      "s_andn2_b64 %[l3], %[l3], %[m3]\n\t"
+      "s_andn2_b64 %[l2], %[l2], %[m2]\n\t"
+      "s_andn2_b64 %[l1], %[l1], %[m1]\n\t"
+      "s_andn2_b64 %[l0], %[l0], %[m0]\n\t"
+      "v_addc_co_u32_e64 %[u], %[cy], %[u], %[u], %[l3]\n\t"
+      "v_addc_co_u32_e64 %[u], %[cy], %[u], %[u], %[l2]\n\t"
+      "v_addc_co_u32_e64 %[u], %[cy], %[u], %[u], %[l1]\n\t"
+      "v_addc_co_u32_e64 %[u], %[cy], %[u], %[u], %[l0]"
+      : [c3] "+v"(c3), [c2] "+v"(c2), [c1] "+v"(c1), [c0] "+v"(c0), [u] "+v"(u), [m3] "=&s"(m3), [m2] "=&s"(m2),
+        [m1] "=&s"(m1), [m0] "=&s"(m0), [l3] "=&s"(l3), [l2] "=&s"(l2), [l1] "=&s"(l1), [l0] "=&s"(l0),
+        [cy] "=&s"(cy)
+      : [s3] "v"(s3), [s2] "v"(s2), [s1] "v"(s1), [s0] "v"(s0), [h3] "v"(hi[3]), [h2] "v"(hi[2]), [h1] "v"(hi[1]),
+        [h0] "v"(hi[0]), [o3] "v"(lo[3]), [o2] "v"(lo[2]), [o1] "v"(lo[1]), [o0] "v"(lo[0]));
 }
 
 template <int MODE>
@@ -891,6 +928,16 @@ void sim_kernel(
             }
             row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
             und[i] = ur | (uc << 16);
+            continue;
+          }
+#endif
+#if CMVE_EPI_T2V_DBL
+          if constexpr (DR && !DC && TN == 4) {  // t2v (the gallery shape): hand-scheduled per column block
+  #pragma unroll
+            for (int j = TN - 1; j >= 0; --j)
+              col4_count_bits(acc[i][j][3], acc[i][j][2], acc[i][j][1], acc[i][j][0], rhi, rlo, c3, c2, c1, c0, u);
+            row_reduce(i, c0 | (c1 << 8) | (c2 << 16) | (c3 << 24));
+            und[i] = u;
             continue;
           }
 #endif
