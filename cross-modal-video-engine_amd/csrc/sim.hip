@@ -458,6 +458,17 @@ constexpr int ring_stages() {
              : (BM == 64 ? CMVE_G64_STAGES : CMVE_G128R_STAGES * (BK / ring_kb<BM, BN, PHASED, NW>()));
 }
 
+// the K-tile depth a kernel instantiation stages: ring_kb, but the 4-wave 128 x 128 batch ring takes CMVE_BATCH4_KB
+// (32: a 32 KiB two-stage ring, three blocks per CU fit the LDS -- a study)
+#ifndef CMVE_BATCH4_KB
+#define CMVE_BATCH4_KB 64
+#endif
+template <int MODE, int BM, int BN, bool PHASED, int NW, bool BATCH>
+constexpr int kernel_kb() {
+  return (BATCH && !PHASED && BM == 128 && BN == 128 && NW == 4 && MODE != CMVE_SIM_BF16X3) ? CMVE_BATCH4_KB
+                                                                                            : ring_kb<BM, BN, PHASED, NW>();
+}
+
 // LDS of the staging buffers of a non-persistent geometry (the launchers' dynamic shared memory)
 template <int MODE, int BM, int BN, bool PHASED, int NW>
 constexpr size_t ring_lds_bytes() {
@@ -570,7 +581,7 @@ void sim_kernel(
   using G = Geo<WM, WN, TM>;
   constexpr int BM = G::BM, BN = G::BN, TN = G::TN, NT = G::NT, NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KB = ring_kb<BM, BN, PHASED, NW>();  // K-tile depth of the staging buffers (BK but the batch ring)
+  constexpr int KB = kernel_kb<MODE, BM, BN, PHASED, NW, BATCH>();  // K-tile depth of the staging buffers
   constexpr int STAGE_BYTES = (int)stage_bytes<MODE, BM, BN, PHASED, KB>();
   constexpr int NS = ring_stages<MODE, BM, BN, PHASED, NW>();
   constexpr int A_BYTES = BM * KB * 2, B_BYTES = BN * KB * 2;
@@ -2690,7 +2701,8 @@ template <int MODE, int WN, int TM, int WM = 4>
 static int launch_rank_batch(const SimArgs* tab, int count, int64_t nq_pad, int64_t ng_pad,
                              hipStream_t stream) {
   using G = Geo<WM, WN, TM>;
-  const size_t lds = ring_lds_bytes<MODE, G::BM, G::BN, false, G::NW>();
+  const size_t lds = (size_t)ring_stages<MODE, G::BM, G::BN, false, G::NW>() *
+                     stage_bytes<MODE, G::BM, G::BN, false, kernel_kb<MODE, G::BM, G::BN, false, G::NW, true>()>();
   static const hipError_t attr_err = hipFuncSetAttribute(
       (const void*)sim_kernel<MODE, EPI_RANK, WM, WN, TM, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)lds);
