@@ -654,16 +654,19 @@ constexpr int FIX_NT = 256;
 // the fix-up of an evaluation with the level-2 planes (d_pad <= 1024): one flat walk over the buckets, TWO listed
 // pairs per wave per step with every level-2 load of both in flight (one round trip of 16 KiB), the directions
 // whose GT score lies outside s2 +- E2 decided there, fp64 (wave_cos64) for the few left
-template <typename TQ, typename TG>
-__device__ __forceinline__ void eval_fix2_walk(const EvalSide& q, const EvalSide& g, const EvalCommon& c) {
-  __shared__ int64_t pre[FIXUP_MAX_BUCKETS_PER_XCD + 1];
+// (vb, nvb: this block among the walk's blocks -- blockIdx.x / gridDim.x, or a role's own numbering in a shared
+// launch; MAXB: the bucket capacity of the LDS prefix)
+template <typename TQ, typename TG, int64_t MAXB = FIXUP_MAX_BUCKETS_PER_XCD>
+__device__ __forceinline__ void eval_fix2_walk(const EvalSide& q, const EvalSide& g, const EvalCommon& c, int64_t vb,
+                                               int64_t nvb) {
+  __shared__ int64_t pre[MAXB + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t nb = c.nb, ldk = c.d_pad;
   if (wave == 0) fixup_prefix(c.cand, nb, c.cap_b, 0, 1, nb, lane, pre);
   __syncthreads();
   const int64_t total = pre[nb];
   const int nw = (int)(blockDim.x >> 6);
-  const int64_t stride = (int64_t)gridDim.x * nw * 2;
+  const int64_t stride = nvb * nw * 2;
   int64_t kb = 0;
   auto entry = [&](int64_t cc) -> uint64_t {  // pair cc of the walk (0: none); cc increases call by call
     if (cc >= total) return 0ull;
@@ -679,7 +682,7 @@ __device__ __forceinline__ void eval_fix2_walk(const EvalSide& q, const EvalSide
     return gld(c.cand + nb + kb * c.cap_b + (cc - pre[kb]));
   };
   const bool dq = q.off != nullptr, dg = g.off != nullptr;
-  for (int64_t c0 = ((int64_t)blockIdx.x * nw + wave) * 2; c0 < total; c0 += stride) {
+  for (int64_t c0 = (vb * nw + wave) * 2; c0 < total; c0 += stride) {
     const uint64_t u[2] = {entry(c0), entry(c0 + 1)};
     int64_t pi[2], pj[2];
     uint32_t fl[2];
@@ -739,7 +742,7 @@ __device__ __forceinline__ void eval_fix_body(const EvalSide& q, const EvalSide&
   EVAL_STAMP(c, 2, 0);
   if (c.dbg & 8) {
   } else if (q.lo16 && g.lo16 && c.nb <= FIXUP_MAX_BUCKETS_PER_XCD) {
-    eval_fix2_walk<TQ, TG>(q, g, c);
+    eval_fix2_walk<TQ, TG>(q, g, c, blockIdx.x, gridDim.x);
   } else {
     fixup_walk<TQ, TG, true>((const TQ*)q.raw, q.ld, q.inv, (const TG*)g.raw, g.ld, g.inv, c.d, q.off ? q.sgt : nullptr,
                              g.off ? g.sgt : nullptr, q.cnt, g.cnt, c.cand, c.nb, c.cap_b,
@@ -952,17 +955,28 @@ template <typename TQ, typename TG, int NM>
 #endif                      // and a launch above 104 fits one wave per SIMD beside the batch rank GEMM's two, not two)
 __global__ __launch_bounds__(PREP_NT, CMVE_PREPFIN_WPE) void eval_prep_fin_batch_kernel(const EvalItem* __restrict__ ptab,
                                                                                     const EvalItem* __restrict__ ftab,
-                                                                                    int nprep, int nfin) {
-  static_assert(PREP_NT == FIN_NT, "one block size for both roles");
+                                                                                    int nprep, int nfin,
+                                                                                    const EvalItem* __restrict__ xtab,
+                                                                                    int nfix) {
+  static_assert(PREP_NT == FIN_NT && PREP_NT == FIX_NT, "one block size for every role");
 #ifdef CMVE_STUDY_PREP_PRIO  // study: the chained prep's waves at a raised priority beside another stream's rank GEMM
   __builtin_amdgcn_s_setprio(CMVE_STUDY_PREP_PRIO);
 #endif
-  if ((int)blockIdx.x < nprep) {
+  const int bx = (int)blockIdx.x;
+  if (bx < nprep) {
     const EvalItem& it = ptab[blockIdx.y];
     eval_prep_pair_f16_body<TQ, TG, NM>(it.q, it.g, it.c, blockIdx.x, nprep);
-  } else if (ftab) {
+  } else if (bx < nprep + nfin) {
     const EvalItem& it = ftab[blockIdx.y];
-    eval_finish_body<TQ, TG, true>(it.q, it.g, it.c, (int)blockIdx.x - nprep, nfin);
+    eval_finish_body<TQ, TG, true>(it.q, it.g, it.c, bx - nprep, nfin);
+  } else {
+#if CMVE_EVAL_FIX_CHAINED  // study: the previous batch's level-2 / fp64 fix-up as a third role of the launch
+    const EvalItem& it = xtab[blockIdx.y];
+    eval_fix2_walk<TQ, TG, EVAL_FIXC_MAXB>(it.q, it.g, it.c, bx - nprep - nfin, nfix);
+#else
+    (void)xtab;
+    (void)nfix;
+#endif
   }
 }
 
@@ -1011,25 +1025,30 @@ static int launch_eval_batch_typed(const EvalSide& q, const EvalSide& g, const E
 
 template <typename TQ, typename TG>
 static int launch_eval_batch_chained_typed(const EvalSide& q, const EvalSide& g, const EvalCommon& c0,
-                                           const EvalItem* ptab, const EvalItem* ftab, int count, hipStream_t s) {
+                                           const EvalItem* ptab, const EvalItem* ftab, int count, hipStream_t s,
+                                           const EvalItem* xtab) {
   const int nm = prep_f16_nm(q, g, c0);
   CMVE_REQUIRE(nm, "launch_eval_batch_chained: the batch does not take the specialised paired prep");
+  CMVE_REQUIRE(!xtab || (CMVE_EVAL_FIX_CHAINED && c0.nb <= EVAL_FIXC_MAXB),
+               "launch_eval_batch_chained: no fix-up role in this build / too many buckets");
   const int nprep = (int)((q.n_pad + PREP_NW - 1) / PREP_NW);
   const int64_t nmax = q.n > g.n ? q.n : g.n;
-  const int nfin = (int)((nmax + FIN_NT - 1) / FIN_NT) + 2;
-  CMVE_PREP_F16(eval_prep_fin_batch_kernel, nm, dim3((unsigned)(nprep + (ftab ? nfin : 0)), (unsigned)count),
-                dim3(PREP_NT), 0u, s, ptab, ftab, nprep, nfin);
+  const int nfin = ftab ? (int)((nmax + FIN_NT - 1) / FIN_NT) + 2 : 0;
+  const int nfix = xtab ? CMVE_FIXB_BLOCKS : 0;
+  CMVE_PREP_F16(eval_prep_fin_batch_kernel, nm, dim3((unsigned)(nprep + nfin + nfix), (unsigned)count),
+                dim3(PREP_NT), 0u, s, ptab, ftab, nprep, nfin, xtab, nfix);
   return check_launch("eval_prep_fin_batch_kernel");
 }
 
 // the specialised paired prep of `ptab` and the finish of `ftab` (nullptr: none) in one launch; both batches have
 // the shapes of q / g / c0 and `count` evaluations
 int launch_eval_batch_chained(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* ptab,
-                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s) {
-  if (!q_f64 && !g_f64) return launch_eval_batch_chained_typed<float, float>(q, g, c0, ptab, ftab, count, s);
-  if (!q_f64 && g_f64) return launch_eval_batch_chained_typed<float, double>(q, g, c0, ptab, ftab, count, s);
-  if (q_f64 && !g_f64) return launch_eval_batch_chained_typed<double, float>(q, g, c0, ptab, ftab, count, s);
-  return launch_eval_batch_chained_typed<double, double>(q, g, c0, ptab, ftab, count, s);
+                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s,
+                              const EvalItem* xtab) {
+  if (!q_f64 && !g_f64) return launch_eval_batch_chained_typed<float, float>(q, g, c0, ptab, ftab, count, s, xtab);
+  if (!q_f64 && g_f64) return launch_eval_batch_chained_typed<float, double>(q, g, c0, ptab, ftab, count, s, xtab);
+  if (q_f64 && !g_f64) return launch_eval_batch_chained_typed<double, float>(q, g, c0, ptab, ftab, count, s, xtab);
+  return launch_eval_batch_chained_typed<double, double>(q, g, c0, ptab, ftab, count, s, xtab);
 }
 
 // whether a batch of these shapes takes launch_eval_batch_chained

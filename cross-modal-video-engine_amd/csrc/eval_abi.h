@@ -69,8 +69,14 @@ struct EvalItem {
   EvalSide q, g;
   EvalCommon c;
 };
+#ifndef CMVE_EVAL_FIX_CHAINED
+#define CMVE_EVAL_FIX_CHAINED 0  // study (with CMVE_EVAL_INLINE_L2=0): a batch's fix-up rides in the next chained launch
+#endif
+constexpr int64_t EVAL_FIXC_MAXB = 1024;  // the chained fix-up role's LDS bucket prefix (a 1k-A evaluation: 256)
+// (xtab: a batch whose fix-up runs as a third role of the launch -- the CMVE_EVAL_FIX_CHAINED study only)
 int launch_eval_batch_chained(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* ptab,
-                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s);
+                              const EvalItem* ftab, int count, int q_f64, int g_f64, hipStream_t s,
+                              const EvalItem* xtab = nullptr);
 bool eval_batch_chainable(const EvalSide& q, const EvalSide& g, const EvalCommon& c0);
 int launch_eval_batch(const EvalSide& q, const EvalSide& g, const EvalCommon& c0, const EvalItem* tab, int count,
                       int q_f64, int g_f64, int phase, hipStream_t s);

@@ -2824,7 +2824,9 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_s
     kev = h->eval_kev[timing_slot];
     for (int k = 0; k < 8; ++k)
       if (!kev[k]) CMVE_HIP(hipEventCreate(&kev[k]));
-    h->eval_no_fix[timing_slot] = !b->fix_launch;
+    // (the CMVE_EVAL_FIX_CHAINED study's batch has no fix-up launch of its own either)
+    h->eval_no_fix[timing_slot] = !b->fix_launch || (chained && b->chainable && CMVE_EVAL_FIX_CHAINED &&
+                                                     b->c0.nb <= cmve::EVAL_FIXC_MAXB);
     h->eval_chained[timing_slot] = chained;
   }
   auto arm = [&](int k) {
@@ -2833,6 +2835,9 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_s
   hipStream_t s = h->stream;
   int st = CMVE_OK;
   const bool fused = chained && b->chainable;  // the prep and the previous batch's finish in one launch
+  // CMVE_EVAL_FIX_CHAINED study (with the fix-up launch form, CMVE_EVAL_INLINE_L2=0): the previous batch's fix-up
+  // rides in this prep launch instead of following its rank GEMM; its finish then follows as a launch of its own
+  const bool fchain = fused && CMVE_EVAL_FIX_CHAINED && b->fix_launch && b->c0.nb <= cmve::EVAL_FIXC_MAXB;
   if (ev) CMVE_HIP(hipEventRecord(ev[0], s));
   if (chained && prev && !fused) {  // (not the specialised prep: the previous batch's finish as a launch of its own,
     // inside the prep's timing span; its own kernel events are not taken -- slot 0's kernel pair times the prep)
@@ -2840,7 +2845,12 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_s
     if (st) return st;
   }
   arm(0);
-  if (fused)
+  if (fchain) {
+    st = cmve::launch_eval_batch_chained(b->sq0, b->sg0, b->c0, b->d_items, nullptr, b->count, b->qf, b->gf, s,
+                                         prev ? prev->d_items : nullptr);
+    if (!st && prev)
+      st = cmve::launch_eval_batch(prev->sq0, prev->sg0, prev->c0, prev->d_items, prev->count, prev->qf, prev->gf, 2, s);
+  } else if (fused)
     st = cmve::launch_eval_batch_chained(b->sq0, b->sg0, b->c0, b->d_items, prev ? prev->d_items : nullptr, b->count,
                                          b->qf, b->gf, s);
   else
@@ -2855,7 +2865,7 @@ static int eval_batch_run(cmve_handle_t h, cmve_eval_batch_t b, int32_t timing_s
   }
   if (st) return st;
   if (ev) CMVE_HIP(hipEventRecord(ev[2], s));
-  if (b->fix_launch) {
+  if (b->fix_launch && !fchain) {
     arm(2);
     st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 1, s);
     if (st) return st;
@@ -2915,6 +2925,10 @@ extern "C" int cmve_eval_batch_finish(cmve_handle_t h, cmve_eval_batch_t b) {
   CMVE_REQUIRE(h && b && b->d_items, "cmve_eval_batch_finish: NULL handle / batch");
   CMVE_REQUIRE(b->pending && b->pending_stream == h->stream,
                "cmve_eval_batch_finish: the batch has no chained run awaiting its finish on this stream");
+  if (CMVE_EVAL_FIX_CHAINED && b->chainable && b->fix_launch && b->c0.nb <= cmve::EVAL_FIXC_MAXB) {
+    const int sf = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 1, h->stream);
+    if (sf) return sf;
+  }
   const int st = cmve::launch_eval_batch(b->sq0, b->sg0, b->c0, b->d_items, b->count, b->qf, b->gf, 2, h->stream);
   if (st) return st;
   b->pending = false;
